@@ -1,0 +1,134 @@
+"""oracle -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding for the CPU restatement in ``oracle/rm_oracle.c`` of the
+reference's per-pixel ray-march pass (common.frag + output_shader.frag +
+template.frag of cahekp/Raymarching).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import this
+package, and only as the checker / CPU baseline: the product path
+(``raymarching_amd``) never touches it.
+
+Pinning: see DESIGN.md "Oracle" -- the restatement is checked against golden
+images that SwiftShader rendered from the reference GLSL in the build
+container (``tests/golden/``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+SCENES = {"S0": 0, "T": 1, "O": 2, "OG": 3}
+
+
+class OracleUniforms(ctypes.Structure):
+    """Mirror of ``oracle_uniforms`` (rm_oracle.c)."""
+
+    _fields_ = [
+        ("res_x", ctypes.c_float), ("res_y", ctypes.c_float),
+        ("mouse_x", ctypes.c_float), ("mouse_y", ctypes.c_float),
+        ("pos_x", ctypes.c_float), ("pos_y", ctypes.c_float), ("pos_z", ctypes.c_float),
+        ("time", ctypes.c_float),
+        ("max_steps", ctypes.c_int32),
+        ("shadow_max_steps", ctypes.c_int32),
+    ]
+
+
+_LIBS: dict[str, ctypes.CDLL] = {}
+
+
+def build(quiet: bool = True) -> None:
+    """Compile oracle/liboracle*.so with the committed Makefile."""
+    out = subprocess.run(["make", "-C", HERE], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+    if not quiet:
+        print(out.stdout)
+
+
+def lib(fast: bool = False) -> ctypes.CDLL:
+    name = "liboracle_fast.so" if fast else "liboracle.so"
+    if name not in _LIBS:
+        path = os.path.join(HERE, name)
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        f32p = ctypes.POINTER(ctypes.c_float)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        up = ctypes.POINTER(OracleUniforms)
+        L.oracle_render.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, f32p, u32p]
+        L.oracle_render.restype = ctypes.c_int
+        L.oracle_render_rows.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, i32p,
+                                         ctypes.c_int, f32p, u32p]
+        L.oracle_render_rows.restype = ctypes.c_int
+        for fn in ("oracle_scene_dist", "oracle_normal"):
+            getattr(L, fn).argtypes = [ctypes.c_int, up, f32p, ctypes.c_int, f32p]
+            getattr(L, fn).restype = ctypes.c_int
+        for fn, n in (("oracle_glsl_mod", 2), ("oracle_glsl_smoothstep", 3), ("oracle_sdbox", 6),
+                      ("oracle_sphere", 7), ("oracle_cube", 7), ("oracle_menger", 3),
+                      ("oracle_smin_cubic", 3), ("oracle_hash11", 1)):
+            getattr(L, fn).argtypes = [ctypes.c_float] * n
+            getattr(L, fn).restype = ctypes.c_float
+        _LIBS[name] = L
+    return _LIBS[name]
+
+
+def uniforms(W, H, pos=(2.0, 3.0, 3.0), mouse=(0.0, 0.0), time=0.0, max_steps=128,
+             shadow_max_steps=0, res=None) -> OracleUniforms:
+    rx, ry = (W, H) if res is None else res
+    return OracleUniforms(float(rx), float(ry), float(mouse[0]), float(mouse[1]), float(pos[0]),
+                          float(pos[1]), float(pos[2]), float(time), int(max_steps),
+                          int(shadow_max_steps))
+
+
+def _p(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def render(scene: str, W: int, H: int, row0: int = 0, nrows: int | None = None, fast=False,
+           **kw):
+    """Render rows [row0,row0+nrows) -> (rgba f32 [nrows,W,4], evals u32 [nrows,W])."""
+    nrows = H - row0 if nrows is None else nrows
+    u = uniforms(W, H, **kw)
+    out = np.zeros((nrows, W, 4), np.float32)
+    ev = np.zeros((nrows, W), np.uint32)
+    rc = lib(fast).oracle_render(SCENES[scene], ctypes.byref(u), W, H, row0, nrows,
+                                 _p(out, ctypes.c_float), _p(ev, ctypes.c_uint32))
+    if rc:
+        raise ValueError(f"oracle_render failed rc={rc}")
+    return out, ev
+
+
+def render_rows(scene: str, W: int, H: int, rows, fast=False, **kw):
+    rows = np.ascontiguousarray(rows, np.int32)
+    u = uniforms(W, H, **kw)
+    out = np.zeros((len(rows), W, 4), np.float32)
+    ev = np.zeros((len(rows), W), np.uint32)
+    rc = lib(fast).oracle_render_rows(SCENES[scene], ctypes.byref(u), W, H, _p(rows, ctypes.c_int32),
+                                      len(rows), _p(out, ctypes.c_float), _p(ev, ctypes.c_uint32))
+    if rc:
+        raise ValueError(f"oracle_render_rows failed rc={rc}")
+    return out, ev
+
+
+def scene_dist(scene: str, pts, **kw):
+    pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+    out = np.zeros(len(pts), np.float32)
+    u = uniforms(1, 1, **kw)
+    lib().oracle_scene_dist(SCENES[scene], ctypes.byref(u), _p(pts, ctypes.c_float), len(pts),
+                            _p(out, ctypes.c_float))
+    return out
+
+
+def normal(scene: str, pts, **kw):
+    pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+    out = np.zeros((len(pts), 3), np.float32)
+    u = uniforms(1, 1, **kw)
+    lib().oracle_normal(SCENES[scene], ctypes.byref(u), _p(pts, ctypes.c_float), len(pts),
+                        _p(out, ctypes.c_float))
+    return out

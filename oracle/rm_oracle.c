@@ -1,0 +1,771 @@
+/*
+ * oracle/rm_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, scalar CPU restatement of the reference's per-pixel ray-march
+ * pass (cahekp/Raymarching: common.frag + output_shader.frag + template.frag),
+ * written line by line against the GLSL so that the HIP product path
+ * (raymarching_amd/csrc) can be checked against it.  Nothing in the product
+ * path links, loads or calls this file: only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg use it, and only as the checker / CPU
+ * baseline.
+ *
+ * Pinning: the reference has no tests or fixtures.  This restatement is
+ * pinned against golden images rendered in-container by SwiftShader from the
+ * reference GLSL itself (tests/golden/make_goldens.py), see DESIGN.md
+ * "Oracle".  GLSL built-ins follow the GLSL 1.30 spec definitions
+ * (min/max/clamp/mix/mod/fract/smoothstep/reflect/refract/normalize).
+ * Transcendentals use libm (the reference's driver precision is unpinned).
+ *
+ * Build: oracle/Makefile (-O2 -ffp-contract=off for parity; an -O3
+ * -march=native variant for the CPU baseline timing).
+ *
+ * Every function cites the reference file:line it restates.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- types */
+
+typedef struct { float x, y; } vec2;
+typedef struct { float x, y, z; } vec3;
+
+/* common.frag:20-35 */
+typedef struct {
+    vec3 diffuse;
+    vec3 specular;
+    float shininess;
+    float reflectivity;
+    float transparency;
+    vec3 absorption;
+    float refraction_index;
+    vec3 emission;
+} Material;
+
+/* common.frag:57-61 */
+typedef struct {
+    float dist;
+    Material mat;
+} SdResult;
+
+enum { SCENE_S0 = 0, SCENE_T = 1, SCENE_O = 2, SCENE_OG = 3 };
+
+/* Uniforms of common.frag:4-7 plus the run-time knobs that replace the
+ * compile-time MAX_MARCHING_STEPS (common.frag:15). Layout mirrored by
+ * tests/oracle.py (ctypes). */
+typedef struct {
+    float res_x, res_y;     /* u_resolution */
+    float mouse_x, mouse_y; /* u_mouse      */
+    float pos_x, pos_y, pos_z; /* u_pos     */
+    float time;             /* u_time       */
+    int32_t max_steps;      /* MAX_MARCHING_STEPS (common.frag:15) */
+    int32_t shadow_max_steps; /* 0 = unbounded, as common.frag:814 */
+} oracle_uniforms;
+
+typedef struct {
+    int scene;
+    oracle_uniforms u;
+    /* transformR's three rotations (common.frag:434-441, 190-227) depend on
+     * uniforms only; their sin/cos are taken once per frame here exactly as
+     * rotationX/Y/Z compute them (radians(), cos(), sin()). */
+    float ry_c, ry_s, rx_c, rx_s, rz_c, rz_s;
+    uint64_t *evals; /* per-thread counter of sceneSDF calls */
+} Ctx;
+
+/* --------------------------------------------------------- GLSL built-ins */
+
+static inline vec3 v3(float x, float y, float z) { vec3 r = {x, y, z}; return r; }
+static inline vec3 v3s(float s) { return v3(s, s, s); }
+static inline vec3 add(vec3 a, vec3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline vec3 sub(vec3 a, vec3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline vec3 mul(vec3 a, vec3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline vec3 muls(vec3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+static inline vec3 divs(vec3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+static inline vec3 neg(vec3 a) { return v3(-a.x, -a.y, -a.z); }
+static inline float dot3(vec3 a, vec3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline float length3(vec3 a) { return sqrtf(dot3(a, a)); }
+static inline vec3 normalize3(vec3 a) { return divs(a, length3(a)); }
+/* GLSL 1.30 spec 8.3: min(x,y) = y < x ? y : x ; max(x,y) = x < y ? y : x */
+static inline float gmin(float x, float y) { return y < x ? y : x; }
+static inline float gmax(float x, float y) { return x < y ? y : x; }
+static inline float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
+static inline float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+static inline vec3 mix3(vec3 x, vec3 y, float a) { return v3(gmix(x.x, y.x, a), gmix(x.y, y.y, a), gmix(x.z, y.z, a)); }
+static inline float gmod(float x, float y) { return x - y * floorf(x / y); }
+static inline float gfract(float x) { return x - floorf(x); }
+static inline float gsmoothstep(float e0, float e1, float x) {
+    float t = gclamp((x - e0) / (e1 - e0), 0.0f, 1.0f);
+    return t * t * (3.0f - 2.0f * t);
+}
+static inline vec3 vabs(vec3 a) { return v3(fabsf(a.x), fabsf(a.y), fabsf(a.z)); }
+static inline vec3 vmax0(vec3 a) { return v3(gmax(a.x, 0.0f), gmax(a.y, 0.0f), gmax(a.z, 0.0f)); }
+/* reflect(I,N) = I - 2.0 * dot(N, I) * N */
+static inline vec3 reflect3(vec3 I, vec3 N) { return sub(I, muls(N, 2.0f * dot3(N, I))); }
+/* refract(I,N,eta): k = 1 - eta*eta*(1 - dot(N,I)*dot(N,I)); k < 0 -> 0 */
+static inline vec3 refract3(vec3 I, vec3 N, float eta) {
+    float d = dot3(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return v3s(0.0f);
+    return sub(muls(I, eta), muls(N, eta * d + sqrtf(k)));
+}
+static inline float radians(float deg) { return deg * 0.017453292519943295f; }
+
+/* ------------------------------------------------------------- constants */
+
+static const float ZNEAR = 0.02f;   /* common.frag:13 */
+static const float ZFAR = 50.0f;    /* common.frag:14 */
+static const float PI = 3.1416f;    /* common.frag:1108 */
+
+/* ---------------------------------------------------------- materials */
+
+/* common.frag:37-53 with ALLOW_MATERIAL_BLENDING defined (output_shader.frag:9) */
+static Material blendMaterial(const Material *a, const Material *b, float k) {
+    Material m;
+    m.diffuse = mix3(a->diffuse, b->diffuse, k);
+    m.specular = mix3(a->specular, b->specular, k);
+    m.shininess = gmix(a->shininess, b->shininess, k);
+    m.reflectivity = gmix(a->reflectivity, b->reflectivity, k);
+    m.transparency = gmix(a->transparency, b->transparency, k);
+    m.absorption = mix3(a->absorption, b->absorption, k);
+    m.refraction_index = gmix(a->refraction_index, b->refraction_index, k);
+    m.emission = mix3(a->emission, b->emission, k);
+    return m;
+}
+
+static Material make_mat(vec3 d, vec3 s, float sh, float refl, float tr, vec3 ab, float ior, vec3 em) {
+    Material m = {d, s, sh, refl, tr, ab, ior, em};
+    return m;
+}
+
+/* output_shader.frag:12 (red), :14 (blue), :15 (mirror) */
+static Material mat_red(void) {
+    return make_mat(v3(0.2f, 0.02f, 0.02f), v3(0.04f, 0.02f, 0.02f), 32.0f, 0.0f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
+}
+static Material mat_blue(int glass) {
+    /* glass != 0 is the test-only variant "OG" that exercises the refraction
+     * path (renderRefraction, output_shader.frag:298-343), which is dead in
+     * the reference scene because every material has transparency 0. */
+    return make_mat(v3(0.02f, 0.02f, 0.2f), v3(0.02f, 0.02f, 0.04f), 32.0f, 0.0f, glass ? 0.9f : 0.0f,
+                    muls(v3(2.0f, 2.0f, 0.75f), 0.2f), 1.52f, v3(0.0f, 0.0f, 100.0f));
+}
+static Material mat_mirror(void) {
+    return make_mat(v3s(0.1f), v3s(0.09f), 64.0f, 0.25f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
+}
+
+/* output_shader.frag:16-28 */
+static Material floorMat(vec3 pos) {
+    vec3 white = v3s(0.3f);
+    vec3 black = v3s(0.025f);
+    float smoothstepSize = 0.005f;
+    float scale = gmax(10.0f, powf(length3(pos), 1.3f));
+    float tx = gsmoothstep(-smoothstepSize, smoothstepSize, sinf(pos.x * PI) / scale);
+    float ty = gsmoothstep(-smoothstepSize, smoothstepSize, sinf(pos.z * PI) / scale);
+    float tile = gmin(gmax(tx, ty), gmax(1.0f - tx, 1.0f - ty));
+    vec3 color = mix3(white, black, tile);
+    return make_mat(color, v3s(0.03f), 128.0f, 0.0f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
+}
+
+/* -------------------------------------------------------- SDF library */
+
+/* common.frag:72-85 (vec2 k form) called through :87-89 with k = vec2(k) */
+static SdResult sminCubic(const SdResult *a, const SdResult *b, float kf) {
+    float kx = gmax(kf, 0.0001f), ky = gmax(kf, 0.0001f);
+    float ad = fabsf(a->dist - b->dist);
+    float hx = gmax(kx - ad, 0.0f) / kx;
+    float hy = gmax(ky - ad, 0.0f) / ky;
+    float mx = hx * hx * hx * 0.5f;
+    float my = hy * hy * hy * 0.5f;
+    float sx = mx * kx * (1.0f / 3.0f);
+    SdResult res;
+    int aCloser = a->dist < b->dist;
+    res.dist = (aCloser ? a->dist : b->dist) - sx;
+    float blendCoeff = aCloser ? my : 1.0f - my;
+    res.mat = blendMaterial(&a->mat, &b->mat, blendCoeff);
+    return res;
+}
+
+/* common.frag:572-575 */
+static float plane(vec3 p) { return p.y; }
+
+/* common.frag:584-587 */
+static float sphere(float sx, float sy, float sz, float sw, vec3 p) {
+    return length3(sub(p, v3(sx, sy, sz))) - sw;
+}
+
+/* common.frag:589-593 */
+static float cube(float sx, float sy, float sz, float sw, vec3 p) {
+    vec3 q = sub(vabs(sub(p, v3(sx, sy, sz))), v3s(sw));
+    return length3(vmax0(q)) + gmin(gmax(q.x, gmax(q.y, q.z)), 0.0f);
+}
+
+/* common.frag:595-600 */
+static float sdBox(vec3 p, vec3 b) {
+    vec3 di = sub(vabs(p), b);
+    float mc = gmax(di.x, gmax(di.y, di.z));
+    return gmin(mc, length3(vmax0(di)));
+}
+
+/* common.frag:654-679; only .x is consumed by the scenes */
+static float mengersponge_x(vec3 p) {
+    float d = sdBox(p, v3s(1.0f));
+    float s = 1.0f;
+    for (int m = 0; m < 3; m++) {
+        vec3 ps = muls(p, s);
+        vec3 a = v3(gmod(ps.x, 2.0f) - 1.0f, gmod(ps.y, 2.0f) - 1.0f, gmod(ps.z, 2.0f) - 1.0f);
+        s *= 3.0f;
+        vec3 r = vabs(sub(v3s(1.0f), muls(vabs(a), 3.0f)));
+        float da = gmax(r.x, r.y);
+        float db = gmax(r.y, r.z);
+        float dc = gmax(r.z, r.x);
+        float c = (gmin(da, gmin(db, dc)) - 1.0f) / s;
+        if (c > d) d = c;
+    }
+    return d;
+}
+
+/* common.frag:434-441: (vec4(p,1) * r_y * r_x * r_z).xyz, each factor a
+ * row-vector x column-major mat4 product (rotationX/Y/Z, :190-227). The
+ * w=1 row contributes exact zeros. */
+static vec3 transformR(const Ctx *C, vec3 p) {
+    /* v * rotationY: cols (c,0,s,0) (0,1,0,0) (-s,0,c,0) */
+    float c = C->ry_c, s = C->ry_s;
+    vec3 q = v3(p.x * c + p.y * 0.0f + p.z * s, p.y, p.x * -s + p.y * 0.0f + p.z * c);
+    /* v * rotationX: cols (1,0,0,0) (0,c,-s,0) (0,s,c,0) */
+    c = C->rx_c; s = C->rx_s;
+    q = v3(q.x, q.x * 0.0f + q.y * c + q.z * -s, q.x * 0.0f + q.y * s + q.z * c);
+    /* v * rotationZ: cols (c,-s,0,0) (s,c,0,0) (0,0,1,0) */
+    c = C->rz_c; s = C->rz_s;
+    q = v3(q.x * c + q.y * -s, q.x * s + q.y * c, q.z);
+    return q;
+}
+
+/* ---------------------------------------------------------- the scenes */
+
+/* Scene S0 (BASELINE config 1): single sphere, red (output_shader.frag:12). */
+static SdResult sceneSDF_S0(const Ctx *C, vec3 p) {
+    (void)C;
+    SdResult r;
+    r.dist = sphere(0.0f, 1.0f, -3.0f, 1.0f, p);
+    r.mat = mat_red();
+    return r;
+}
+
+/* Scene T: template.frag:39-43 repaired: the sponge
+ * distance with the red material. */
+static SdResult sceneSDF_T(const Ctx *C, vec3 p) {
+    SdResult r;
+    r.dist = mengersponge_x(transformR(C, sub(p, v3(0.0f, 3.0f, 0.0f))));
+    r.mat = mat_red();
+    return r;
+}
+
+/* Scene O: output_shader.frag:38-48 */
+static SdResult sceneSDF_O(const Ctx *C, vec3 p) {
+    SdResult d0, d1, d2, d3, t1, t2;
+    d0.dist = mengersponge_x(transformR(C, sub(p, v3(0.0f, 3.0f, 0.0f))));
+    d0.mat = mat_mirror();
+    d1.dist = sphere(3.0f, 2.0f, 3.0f, 1.0f, p);
+    d1.mat = mat_blue(C->scene == SCENE_OG);
+    d2.dist = cube(-5.0f, 4.0f, 5.0f, 1.0f, p);
+    d2.mat = mat_blue(C->scene == SCENE_OG);
+    d3.dist = plane(p);
+    d3.mat = floorMat(p);
+    t1 = sminCubic(&d1, &d2, 0.5f);
+    t2 = sminCubic(&t1, &d3, 0.5f);
+    return sminCubic(&d0, &t2, 0.33f);
+}
+
+static SdResult sceneSDF(const Ctx *C, vec3 p) {
+    (*C->evals)++;
+    switch (C->scene) {
+    case SCENE_S0: return sceneSDF_S0(C, p);
+    case SCENE_T: return sceneSDF_T(C, p);
+    default: return sceneSDF_O(C, p);
+    }
+}
+
+/* ------------------------------------------------------- marching etc. */
+
+/* common.frag:697-708 */
+static vec3 getNormalFast(const Ctx *C, vec3 p) {
+    const float h = 0.001f;
+    const vec3 k0 = v3(1.0f, -1.0f, -1.0f);
+    const vec3 k1 = v3(-1.0f, -1.0f, 1.0f);
+    const vec3 k2 = v3(-1.0f, 1.0f, -1.0f);
+    const vec3 k3 = v3(1.0f, 1.0f, 1.0f);
+    float d0 = sceneSDF(C, add(p, muls(k0, h))).dist;
+    float d1 = sceneSDF(C, add(p, muls(k1, h))).dist;
+    float d2 = sceneSDF(C, add(p, muls(k2, h))).dist;
+    float d3 = sceneSDF(C, add(p, muls(k3, h))).dist;
+    return normalize3(add(add(add(muls(k0, d0), muls(k1, d1)), muls(k2, d2)), muls(k3, d3)));
+}
+
+/* common.frag:710-713 */
+static float lambert(vec3 lightDir, vec3 n) { return gclamp(dot3(n, lightDir), 0.0f, 1.0f); }
+
+/* common.frag:730-754.  N is passed in: the reference recomputes
+ * getNormalFast(p) here (:733) at the very p whose normal the caller already
+ * holds; a pure function of p, so the value is identical and the 4 repeated
+ * sceneSDF calls are elided (and not counted) in both oracle and HIP path. */
+static vec3 phongContribForLight(vec3 k_d, vec3 k_s, float alpha, vec3 p, vec3 eye,
+                                 vec3 lightPos, vec3 lightIntensity, vec3 N) {
+    vec3 L = normalize3(sub(lightPos, p));
+    vec3 V = normalize3(sub(eye, p));
+    vec3 R = normalize3(reflect3(neg(L), N));
+    float dotLN = dot3(L, N);
+    float dotRV = dot3(R, V);
+    if (dotLN < 0.0f) return v3s(0.0f);
+    if (dotRV < 0.0f) return mul(lightIntensity, muls(k_d, dotLN));
+    return mul(lightIntensity, add(muls(k_d, dotLN), muls(k_s, powf(dotRV, alpha))));
+}
+
+/* common.frag:810-831.  max_steps == 0: unbounded, as the reference. */
+static float softshadow2(const Ctx *C, vec3 ro, vec3 rd, float mint, float maxt, float k) {
+    float res = 1.0f;
+    float ph = 1e20f;
+    int it = 0;
+    for (float t = mint; t < maxt;) {
+        if (C->u.shadow_max_steps > 0 && it++ >= C->u.shadow_max_steps) break;
+        float h = sceneSDF(C, add(ro, muls(rd, t))).dist;
+        if (h < 0.001f) return 0.0f;
+        float y = h * h / (2.0f * ph);
+        float d = sqrtf(h * h - y * y);
+        res = gmin(res, k * d / gmax(0.0f, t - y));
+        ph = h;
+        t += h * 0.1f + 0.001f;
+    }
+    return res;
+}
+
+/* common.frag:850-866 (_AOSteps = 4, _AOStepSize = 0.2) */
+static float ambientOcclusionReal(const Ctx *C, vec3 pos, vec3 normal) {
+    float sum = 0.0f;
+    float maxSum = 0.0f;
+    for (int i = 0; i < 4; i++) {
+        vec3 p = add(pos, muls(muls(normal, (float)(i + 1)), 0.2f));
+        sum += 1.0f / powf(2.0f, (float)i) * sceneSDF(C, p).dist;
+        maxSum += 1.0f / powf(2.0f, (float)i) * (float)(i + 1) * 0.2f;
+    }
+    return sum / maxSum;
+}
+
+/* common.frag:879-901 */
+static SdResult castRayD(const Ctx *C, vec3 ro, vec3 rd) {
+    SdResult res;
+    memset(&res, 0, sizeof(res));
+    float depth = ZNEAR;
+    for (int i = 0; i < C->u.max_steps; i++) {
+        res = sceneSDF(C, add(ro, muls(rd, depth)));
+        if (res.dist < 0.001f * depth) {
+            res.dist = depth;
+            return res;
+        }
+        depth += res.dist;
+        if (depth >= ZFAR) {
+            res.dist = -1.0f;
+            return res;
+        }
+    }
+    return res;
+}
+
+/* common.frag:903-925 */
+static SdResult castRayDI(const Ctx *C, vec3 ro, vec3 rd) {
+    SdResult res;
+    memset(&res, 0, sizeof(res));
+    float depth = ZNEAR;
+    for (int i = 0; i < C->u.max_steps; i++) {
+        res = sceneSDF(C, add(ro, muls(rd, depth)));
+        if (-res.dist < 0.001f * depth) {
+            res.dist = depth;
+            return res;
+        }
+        depth -= res.dist;
+        if (depth >= ZFAR) {
+            res.dist = -1.0f;
+            return res;
+        }
+    }
+    return res;
+}
+
+/* common.frag:931-954 */
+static vec3 castRay(const Ctx *C, vec3 ro, vec3 rd) {
+    float depth = ZNEAR;
+    vec3 p = add(ro, muls(rd, depth));
+    for (int i = 0; i < C->u.max_steps; i++) {
+        float dist = sceneSDF(C, p).dist;
+        if (dist < 0.001f) return p;
+        depth += dist;
+        p = add(ro, muls(rd, depth));
+        if (depth >= ZFAR) return add(ro, muls(rd, ZFAR));
+    }
+    return p;
+}
+
+/* common.frag:991-1002 (getColor :983-986 is white).  The reference's
+ * `nr = getNormalFast(pr)` (:995) is dead code and is not evaluated. */
+static vec3 getColorReflect(const Ctx *C, vec3 p, vec3 n, vec3 rd) {
+    vec3 reflect_dir = reflect3(rd, n);
+    vec3 pr = castRay(C, add(p, muls(reflect_dir, 0.01f)), reflect_dir);
+    vec3 c = v3s(1.0f);
+    c = muls(c, gclamp(length3(sub(pr, p)) / 3.0f, 0.0f, 1.0f));
+    return c;
+}
+
+/* common.frag:1032-1042 */
+static vec3 applyScattering(vec3 color, vec3 ro, vec3 p, vec3 fog_color, vec3 be, vec3 bi) {
+    float d = 1.0f - gclamp(length3(sub(p, ro)) / ZFAR, 0.0f, 1.0f);
+    vec3 ext = v3(expf(-d * be.x), expf(-d * be.y), expf(-d * be.z));
+    vec3 ins = v3(expf(-d * bi.x), expf(-d * bi.y), expf(-d * bi.z));
+    return add(mul(color, sub(v3s(1.0f), ext)), mul(fog_color, ins));
+}
+
+/* common.frag:1044-1051 */
+static vec3 tonemap(vec3 color) {
+    vec3 col = v3(color.x * 2.0f / (1.0f + color.x), color.y * 2.0f / (1.0f + color.y),
+                  color.z * 2.0f / (1.0f + color.z));
+    col = v3(powf(col.x, 0.4545f), powf(col.y, 0.4545f), powf(col.z, 0.4545f));
+    col = v3(powf(col.x, 0.85f), powf(col.y, 0.97f), powf(col.z, 1.0f));
+    col = v3(col.x * 0.5f + 0.5f * col.x * col.x * (3.0f - 2.0f * col.x),
+             col.y * 0.5f + 0.5f * col.y * col.y * (3.0f - 2.0f * col.y),
+             col.z * 0.5f + 0.5f * col.z * col.z * (3.0f - 2.0f * col.z));
+    return col;
+}
+
+/* common.frag:1067-1070 */
+static vec3 contrast(vec3 c) {
+    return v3(gsmoothstep(0.15f, 1.1f, c.x), gsmoothstep(0.15f, 1.1f, c.y), gsmoothstep(0.15f, 1.1f, c.z));
+}
+
+/* common.frag:1072-1075 (amount = 0.1, the default the callers use) */
+static vec3 vignette(vec3 color, vec2 uv) {
+    float amount = 0.1f;
+    return muls(color, 0.5f + 0.5f * powf(16.0f * uv.x * uv.y * (1.0f - uv.x) * (1.0f - uv.y), amount));
+}
+
+/* ------------------------------------------------ scene O (output_shader) */
+
+static const vec3 FOG = {0.34f, 0.435f, 0.57f};
+
+/* output_shader.frag:54-59 */
+static float Hash11(float p) {
+    vec3 p3 = v3(gfract(p * 443.897f), gfract(p * 443.897f), gfract(p * 443.897f));
+    float dd = dot3(p3, add(v3(p3.y, p3.z, p3.x), v3s(19.19f)));
+    p3 = add(p3, v3s(dd));
+    return gfract((p3.x + p3.y) * p3.z);
+}
+
+/* output_shader.frag:61-66 */
+static vec3 Hash33(vec3 p3) {
+    p3 = v3(gfract(p3.x * 443.897f), gfract(p3.y * 441.423f), gfract(p3.z * 437.195f));
+    float dd = dot3(p3, add(v3(p3.y, p3.x, p3.z), v3s(19.19f)));
+    p3 = add(p3, v3s(dd));
+    /* fract((p3.xxy + p3.yxx) * p3.zyx) */
+    return v3(gfract((p3.x + p3.y) * p3.z), gfract((p3.x + p3.x) * p3.y), gfract((p3.y + p3.x) * p3.x));
+}
+
+/* output_shader.frag:70-73 */
+static vec3 reflectVector(vec3 v, vec3 n) { return sub(v, muls(muls(n, 2.0f), gmin(0.0f, dot3(v, n)))); }
+
+/* output_shader.frag:77-81 */
+static vec3 GenerateSampleVector(vec3 norm, float i) {
+    vec3 randDir = normalize3(sub(Hash33(add(norm, v3s(i))), v3s(0.5f)));
+    return reflectVector(randDir, norm);
+}
+
+/* output_shader.frag:85-116 */
+static float CalculateThickness(const Ctx *C, vec3 pos, vec3 norm) {
+    const float SSSSampleDepth = 1.0f;
+    const float SSSThicknessSamples = 32.0f;
+    const float SSSThicknessSamplesI = 0.03125f;
+    float thickness = 0.0f;
+    for (float i = 0.0f; i < SSSThicknessSamples; ++i) {
+        float sampleLength = Hash11(i) * SSSSampleDepth;
+        vec3 sampleDir = GenerateSampleVector(neg(norm), i);
+        thickness += sampleLength + sceneSDF(C, add(pos, muls(sampleDir, sampleLength))).dist;
+    }
+    return gclamp(thickness * SSSThicknessSamplesI, 0.0f, 1.0f);
+}
+
+/* output_shader.frag:127-176 (Attenuation :161 is computed but unused) */
+static vec3 light(const Ctx *C, const Material *mat, vec3 ro, vec3 rd, vec3 p, vec3 n, vec3 phongN) {
+    vec3 lightPos = v3(20.0f, 50.0f, 0.0f);
+    vec3 lightDir = normalize3(sub(lightPos, p));
+    float occ = ambientOcclusionReal(C, p, n);
+    float sha = softshadow2(C, p, lightDir, 0.01f, length3(sub(lightPos, p)), 4.0f);
+    float sky = gclamp(0.5f + 0.5f * n.y, 0.0f, 1.0f);
+    float ind = gclamp(dot3(n, normalize3(mul(lightDir, v3(-1.0f, 0.0f, -1.0f)))), 0.0f, 1.0f);
+    vec3 shading = phongContribForLight(v3(1.64f, 1.27f, 0.99f), mat->specular, mat->shininess, p, ro,
+                                        lightPos, v3s(1.0f), phongN);
+    shading = mul(shading, v3(powf(sha, 1.0f), powf(sha, 1.2f), powf(sha, 1.5f)));
+    shading = add(shading, muls(muls(v3(0.16f, 0.20f, 0.28f), sky), occ));
+    shading = add(shading, muls(muls(v3(0.40f, 0.28f, 0.20f), ind), occ));
+    float SSSAmbient = 0.3f;
+    float SSSDistortion = 0.6f;
+    float SSSPower = 1.1f;
+    float SSSScale = 0.3f;
+    float thickness = CalculateThickness(C, p, n);
+    vec3 toEye = neg(rd);
+    vec3 SSSLight = add(lightDir, muls(n, SSSDistortion));
+    float SSSDot = powf(gclamp(dot3(toEye, neg(SSSLight)), 0.0f, 1.0f), SSSPower) * SSSScale;
+    float SSS = (SSSDot + SSSAmbient) * thickness;
+    shading = add(shading, v3s(SSS));
+    vec3 color = add(mul(mat->diffuse, shading), mat->emission);
+    color = applyScattering(color, ro, p, FOG, v3s(2.0f), v3s(2.0f));
+    return color;
+}
+
+/* output_shader.frag:178-182 */
+static vec3 background(vec3 ro, vec3 rd) {
+    return applyScattering(v3s(0.0f), ro, add(ro, muls(rd, ZFAR)), FOG, v3s(2.0f), v3s(2.0f));
+}
+
+/* output_shader.frag:218-230 */
+static float fresnelReflection(float n2, vec3 normal, vec3 incident, float reflectivity) {
+    float r0 = (1.0f - n2) / (1.0f + n2);
+    r0 *= r0;
+    float x = 1.0f + dot3(normal, incident);
+    float r = r0 + (1.0f - r0) * x * x * x * x * x;
+    r = (1.0f - reflectivity) * r + reflectivity;
+    return r;
+}
+
+/* output_shader.frag:246-262 (MAX_REFLECTIONS == 1) */
+static vec3 renderReflection(const Ctx *C, vec3 ro, vec3 rd) {
+    SdResult sd = castRayD(C, ro, rd);
+    if (sd.dist > 0.0f) {
+        vec3 p = add(ro, muls(rd, sd.dist));
+        vec3 n = getNormalFast(C, p);
+        return light(C, &sd.mat, ro, rd, p, n, n);
+    }
+    return background(ro, rd);
+}
+
+/* output_shader.frag:298-343 (MAX_REFRACTIONS 4) */
+static vec3 renderRefraction(const Ctx *C, vec3 ro, vec3 rd, vec3 absorption) {
+    vec3 color = v3s(0.0f);
+    float invert = -1.0f;
+    float absorb_dist = 0.0f;
+    for (int i = 0; i < 4; i++) {
+        SdResult sd;
+        if (invert < 0.0f) sd = castRayDI(C, ro, rd);
+        else sd = castRayD(C, ro, rd);
+        if (invert < 0.0f) absorb_dist += sd.dist;
+        if (sd.dist < 0.0f) {
+            if (invert > 0.0f) color = add(color, background(ro, rd));
+            break;
+        }
+        vec3 p = add(ro, muls(rd, sd.dist));
+        vec3 g = getNormalFast(C, p);
+        vec3 n = muls(g, invert);
+        vec3 ref = reflect3(rd, n);
+        /* light()'s phong recomputes getNormalFast(p) == g (not n) */
+        color = add(color, light(C, &sd.mat, ro, ref, p, n, g));
+        if (invert > 0.0f) break;
+        float ior = invert < 0.0f ? sd.mat.refraction_index : 1.0f / sd.mat.refraction_index;
+        vec3 raf = refract3(rd, n, ior);
+        int tif = raf.x == 0.0f && raf.y == 0.0f && raf.z == 0.0f;
+        rd = tif ? ref : raf;
+        ro = add(p, muls(rd, 0.01f / fabsf(dot3(rd, n))));
+        invert = tif ? invert : invert * -1.0f;
+    }
+    return mul(color, v3(expf(-absorption.x * absorb_dist), expf(-absorption.y * absorb_dist),
+                         expf(-absorption.z * absorb_dist)));
+}
+
+/* output_shader.frag:348-385 */
+static vec3 render_O(const Ctx *C, vec3 ro, vec3 rd) {
+    SdResult sd = castRayD(C, ro, rd);
+    if (sd.dist > 0.0f) {
+        vec3 p = add(ro, muls(rd, sd.dist));
+        vec3 n = getNormalFast(C, p);
+        vec3 color = light(C, &sd.mat, ro, rd, p, n, n);
+        float reflect_factor = fresnelReflection(sd.mat.refraction_index, n, rd,
+                                                 sd.mat.transparency > 0.0f ? 0.0f : sd.mat.reflectivity);
+        float refract_factor = 1.0f - reflect_factor;
+        if (sd.mat.reflectivity > 0.0f) {
+            vec3 reflected_rd = reflect3(rd, n);
+            vec3 rc = renderReflection(C, add(p, muls(reflected_rd, 0.001f)), reflected_rd);
+            color = add(color, muls(muls(rc, reflect_factor), sd.mat.reflectivity));
+        }
+        if (sd.mat.transparency > 0.0f) {
+            vec3 refracted_rd = refract3(rd, n, 1.0f / sd.mat.refraction_index);
+            vec3 rc = renderRefraction(C, add(p, muls(refracted_rd, 0.001f)), refracted_rd, sd.mat.absorption);
+            color = add(color, muls(muls(rc, refract_factor), sd.mat.transparency));
+        }
+        return color;
+    }
+    return background(ro, rd);
+}
+
+/* ---------------------------------------------------- scene T (template) */
+
+/* template.frag:45-76 */
+static vec3 render_T(const Ctx *C, vec3 ro, vec3 rd) {
+    vec3 p = castRay(C, ro, rd);
+    vec3 n = getNormalFast(C, p);
+    vec3 c = getColorReflect(C, p, n, rd);
+    vec3 lightPos = v3(20.0f, 50.0f, 0.0f);
+    vec3 lightDir = normalize3(sub(lightPos, p));
+    float occ = ambientOcclusionReal(C, p, n);
+    float sha = softshadow2(C, p, lightDir, 0.01f, length3(sub(lightPos, p)), 4.0f);
+    float sky = gclamp(0.5f + 0.5f * n.y, 0.0f, 1.0f);
+    float ind = gclamp(dot3(n, normalize3(mul(lightDir, v3(-1.0f, 0.0f, -1.0f)))), 0.0f, 1.0f);
+    float fre = powf(gclamp(1.0f + dot3(n, rd), 0.0f, 1.0f), 2.0f);
+    vec3 shading = phongContribForLight(v3(1.64f, 1.27f, 0.99f), v3(1.0f, 1.0f, 0.0f), 1280.0f, p, ro, lightPos,
+                                        v3s(1.0f), n);
+    shading = mul(shading, v3(powf(sha, 1.0f), powf(sha, 1.2f), powf(sha, 1.5f)));
+    shading = add(shading, muls(muls(v3(0.16f, 0.20f, 0.28f), sky), occ));
+    shading = add(shading, muls(muls(v3(0.40f, 0.28f, 0.20f), ind), occ));
+    shading = add(shading, muls(muls(v3s(1.0f), fre), occ));
+    c = mul(c, shading);
+    c = applyScattering(c, ro, p, FOG, v3s(2.0f), v3s(2.0f));
+    return c;
+}
+
+/* ------------------------------------------- scene S0 (BASELINE config 1) */
+
+/* castRayD + tetrahedral normal + 0.1-ambient lambert from the scene light;
+ * background() on a miss.  Defined in DESIGN.md (not a reference scene). */
+static vec3 render_S0(const Ctx *C, vec3 ro, vec3 rd) {
+    SdResult sd = castRayD(C, ro, rd);
+    if (sd.dist > 0.0f) {
+        vec3 p = add(ro, muls(rd, sd.dist));
+        vec3 n = getNormalFast(C, p);
+        vec3 lightDir = normalize3(sub(v3(20.0f, 50.0f, 0.0f), p));
+        return muls(sd.mat.diffuse, 0.1f + lambert(lightDir, n));
+    }
+    return background(ro, rd);
+}
+
+/* ------------------------------------------------------------ main() */
+
+/* output_shader.frag:388-420 / template.frag:78-99, at pixel (col,row) of a
+ * W x H target: gl_TexCoord = ((col+.5)/W, (row+.5)/H) (row 0 first in
+ * memory). */
+static void shade_pixel(const Ctx *C, int W, int H, int col, int row, float *out4) {
+    vec2 tc = {((float)col + 0.5f) / (float)W, ((float)row + 0.5f) / (float)H};
+    vec2 uv = {(tc.x - 0.5f) * C->u.res_x / C->u.res_y, (tc.y - 0.5f) * C->u.res_y / C->u.res_y};
+    vec3 ro = v3(C->u.pos_x, C->u.pos_y, C->u.pos_z);
+    vec3 rd = normalize3(v3(uv.x, -uv.y, -1.0f));
+    /* rd.yz *= rot(-u_mouse.y); rd.xz *= rot(u_mouse.x)   (common.frag:1088-1092) */
+    float a = -C->u.mouse_y;
+    float s = sinf(a), c = cosf(a);
+    float y = rd.y * c + rd.z * -s;
+    float z = rd.y * s + rd.z * c;
+    rd.y = y; rd.z = z;
+    a = C->u.mouse_x;
+    s = sinf(a); c = cosf(a);
+    float x = rd.x * c + rd.z * -s;
+    z = rd.x * s + rd.z * c;
+    rd.x = x; rd.z = z;
+    vec3 col3;
+    switch (C->scene) {
+    case SCENE_S0: col3 = render_S0(C, ro, rd); break;
+    case SCENE_T: col3 = render_T(C, ro, rd); break;
+    default: col3 = render_O(C, ro, rd); break;
+    }
+    col3 = tonemap(col3);
+    col3 = contrast(col3);
+    col3 = vignette(col3, tc);
+    out4[0] = col3.x; out4[1] = col3.y; out4[2] = col3.z; out4[3] = 1.0f;
+}
+
+static void init_ctx(Ctx *C, int scene, const oracle_uniforms *u) {
+    memset(C, 0, sizeof(*C));
+    C->scene = scene;
+    C->u = *u;
+    /* transformR(p - vec3(0,3,0), vec3(180, u_time * 2, 0)) (output_shader.frag:42,
+     * template.frag:41): rotationY(-rot.y), rotationX(-rot.x), rotationZ(-rot.z) */
+    float rot_x = 180.0f, rot_y = u->time * 2.0f, rot_z = 0.0f;
+    float ay = radians(-rot_y), ax = radians(-rot_x), az = radians(-rot_z);
+    C->ry_c = cosf(ay); C->ry_s = sinf(ay);
+    C->rx_c = cosf(ax); C->rx_s = sinf(ax);
+    C->rz_c = cosf(az); C->rz_s = sinf(az);
+}
+
+/* ---------------------------------------------------------- exported API */
+
+/* Render rows [row0, row0+nrows) of a W x H frame into out (nrows*W*4 f32,
+ * row-major RGBA).  evals (optional, nrows*W u32) gets the per-pixel count of
+ * sceneSDF calls.  Rows are distributed dynamically over OpenMP threads. */
+int oracle_render(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, float *out,
+                  uint32_t *evals) {
+    if (!u || !out || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H) return 1;
+    if (scene < SCENE_S0 || scene > SCENE_OG) return 2;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; r++) {
+        Ctx C;
+        uint64_t cnt = 0;
+        init_ctx(&C, scene, u);
+        C.evals = &cnt;
+        for (int x = 0; x < W; x++) {
+            uint64_t before = cnt;
+            shade_pixel(&C, W, H, x, row0 + r, out + ((size_t)r * W + x) * 4);
+            if (evals) evals[(size_t)r * W + x] = (uint32_t)(cnt - before);
+        }
+    }
+    return 0;
+}
+
+/* Render an explicit list of rows (used for strided CPU-baseline samples). */
+int oracle_render_rows(int scene, const oracle_uniforms *u, int W, int H, const int32_t *rows, int nrows,
+                       float *out, uint32_t *evals) {
+    if (!u || !out || !rows || W <= 0 || H <= 0 || nrows < 0) return 1;
+    if (scene < SCENE_S0 || scene > SCENE_OG) return 2;
+    for (int i = 0; i < nrows; i++)
+        if (rows[i] < 0 || rows[i] >= H) return 1;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; r++) {
+        Ctx C;
+        uint64_t cnt = 0;
+        init_ctx(&C, scene, u);
+        C.evals = &cnt;
+        for (int x = 0; x < W; x++) {
+            uint64_t before = cnt;
+            shade_pixel(&C, W, H, x, rows[r], out + ((size_t)r * W + x) * 4);
+            if (evals) evals[(size_t)r * W + x] = (uint32_t)(cnt - before);
+        }
+    }
+    return 0;
+}
+
+/* Scene distance at explicit points (n x 3 in, n out) — KAT entry. */
+int oracle_scene_dist(int scene, const oracle_uniforms *u, const float *pts, int n, float *out) {
+    Ctx C;
+    uint64_t cnt = 0;
+    init_ctx(&C, scene, u);
+    C.evals = &cnt;
+    for (int i = 0; i < n; i++) out[i] = sceneSDF(&C, v3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2])).dist;
+    return 0;
+}
+
+/* Normal at explicit points — KAT entry. */
+int oracle_normal(int scene, const oracle_uniforms *u, const float *pts, int n, float *out) {
+    Ctx C;
+    uint64_t cnt = 0;
+    init_ctx(&C, scene, u);
+    C.evals = &cnt;
+    for (int i = 0; i < n; i++) {
+        vec3 g = getNormalFast(&C, v3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]));
+        out[3 * i] = g.x; out[3 * i + 1] = g.y; out[3 * i + 2] = g.z;
+    }
+    return 0;
+}
+
+/* Built-in KATs: name -> f(x, y, z) */
+float oracle_glsl_mod(float x, float y) { return gmod(x, y); }
+float oracle_glsl_smoothstep(float a, float b, float x) { return gsmoothstep(a, b, x); }
+float oracle_sdbox(float px, float py, float pz, float bx, float by, float bz) { return sdBox(v3(px, py, pz), v3(bx, by, bz)); }
+float oracle_sphere(float px, float py, float pz, float sx, float sy, float sz, float sw) { return sphere(sx, sy, sz, sw, v3(px, py, pz)); }
+float oracle_cube(float px, float py, float pz, float sx, float sy, float sz, float sw) { return cube(sx, sy, sz, sw, v3(px, py, pz)); }
+float oracle_menger(float px, float py, float pz) { return mengersponge_x(v3(px, py, pz)); }
+float oracle_smin_cubic(float a, float b, float k) {
+    SdResult ra, rb;
+    memset(&ra, 0, sizeof(ra)); memset(&rb, 0, sizeof(rb));
+    ra.dist = a; rb.dist = b;
+    return sminCubic(&ra, &rb, k).dist;
+}
+float oracle_hash11(float p) { return Hash11(p); }

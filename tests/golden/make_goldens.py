@@ -1,0 +1,384 @@
+#!/usr/bin/env python3
+"""Generate golden images by running the REFERENCE GLSL itself (test data only).
+
+Runs in the build container, never on the GPU box: it reads the reference
+shaders from /root/reference, inlines ``#include`` exactly as
+``ShaderLoader::preprocess`` does (source/shader_loader.cpp:22-81), applies the
+mechanical GLSL-1.30 -> GLSL-ES-3.00 rewrites of SURVEY.md Appendix A (no
+semantic change; the ``template.frag`` repair that defines scene T is the one
+semantic edit, also Appendix A), compiles the result with the SwiftShader
+GLES3 implementation bundled in the ``kaleido`` wheel, renders full-screen
+passes into an RGBA32F FBO and stores the pixels.  The adapted shader text
+lives only in memory; only the rendered numbers are committed
+(``tests/golden/*.npz``).
+
+Each fixture holds:
+  rgba   float32 [H,W,4]   pre-quantisation ``gl_FragColor`` (row 0 = tc.y 0.5/H)
+  evals  int32   [H,W]     sceneSDF calls per pixel, counting as the build
+                           does: the dead ``nr`` normal of getColorReflect
+                           (common.frag:995) and phongContribForLight's repeat
+                           of the caller's normal (common.frag:733) excluded.
+  meta   json string       scene, W, H, pose, max_steps
+
+Usage: python tests/golden/make_goldens.py [--ref /root/reference]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import re
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from raymarching_amd.poses import POSES, S0_POSE  # noqa: E402
+
+SS = "/usr/local/lib/python3.10/dist-packages/kaleido/executable/bin/swiftshader/"
+
+# ----------------------------------------------------------- shader source
+
+
+def preprocess(path: str, root: str) -> str:
+    """Same semantics as ShaderLoader::preprocess: an ``#include`` not preceded
+    by ``//`` on its line pulls in the named file (no include guards)."""
+    out = []
+    with open(path) as f:
+        for line in f.read().split("\n"):
+            k = line.find("#include")
+            if k != -1 and (k == 0 or line.rfind("//", 0, k) == -1):
+                m = re.search(r'["<]([^">]*)[">]', line[k + 8:])
+                out.append(preprocess(os.path.join(root, m.group(1)), root))
+                continue
+            out.append(line)
+    return "\n".join(out)
+
+
+def must_sub(pat, rep, s, count=0, regex=False):
+    new = re.sub(pat, rep, s, count=count) if regex else s.replace(pat, rep) if count == 0 else s.replace(pat, rep, count)
+    if new == s:
+        raise RuntimeError(f"rewrite did not apply: {pat!r}")
+    return new
+
+
+def es3_rewrite(src: str) -> str:
+    """SURVEY Appendix A mechanical rewrites (GLSL 1.30 leniencies -> ES 3.00)."""
+    s = src
+    s = re.sub(r"^\s*#version.*$", "", s, flags=re.M)
+    s = must_sub("const float ZFAR = 50;", "const float ZFAR = 50.0;", s)
+    # default arguments (the reference call sites pass every argument)
+    s = must_sub("float k = 32)", "float k)", s)
+    s = must_sub("in float h = 0.1)", "in float h)", s)
+    s = must_sub("float maxt, float k = 2)", "float maxt, float k)", s)
+    s = must_sub("in vec3 be = vec3(2.0), in vec3 bi = vec3(2.0))", "in vec3 be, in vec3 bi)", s)
+    s = must_sub("float value = 0.9)", "float value)", s)
+    s = must_sub("float value = 0.85)", "float value)", s)
+    s = must_sub("float amount = 0.1)", "float amount)", s)
+    # implicit int -> float
+    s = must_sub(r"\b1/scale", "1.0/scale", s, regex=True)
+    s = must_sub("length(max(q, 0)) + min(max(q.x, max(q.y, q.z)), 0)",
+                 "length(max(q, 0.0)) + min(max(q.x, max(q.y, q.z)), 0.0)", s)
+    s = must_sub("float s = (p<0)?-1:1;", "float s = (p<0.0)?-1.0:1.0;", s)
+    s = must_sub("if (t < 0) {", "if (t < 0.0) {", s)
+    s = must_sub("(2*t)*planeNormal", "(2.0*t)*planeNormal", s)
+    s = must_sub("return (t<0)?-1:1;", "return (t<0.0)?-1.0:1.0;", s)
+    s = must_sub("(1 - a) * d2", "(1.0 - a) * d2", s)
+    s = must_sub("const float _AOSteps = 4;", "const int _AOSteps = 4;", s)
+    s = must_sub("float sum    = 0;", "float sum    = 0.0;", s)
+    s = must_sub("float maxSum = 0;", "float maxSum = 0.0;", s)
+    s = must_sub("normal * (i+1) * _AOStepSize", "normal * float(i+1) * _AOStepSize", s)
+    s = must_sub("1. / pow(2., i) * sceneSDF(p).dist", "1. / pow(2., float(i)) * sceneSDF(p).dist", s)
+    s = must_sub("1. / pow(2., i) * (i+1) * _AOStepSize", "1. / pow(2., float(i)) * float(i+1) * _AOStepSize", s)
+    # step counting (fixture-only instrumentation): skip the dead nr normal
+    # and phong's repeat of the caller's normal, as the build does
+    s = must_sub("vec3 N = getNormalFast(p);", "g_cnt_off++; vec3 N = getNormalFast(p); g_cnt_off--;", s)
+    s = must_sub("vec3 nr = getNormalFast(pr);\n    \n\t// return simple depth texture",
+                 "g_cnt_off++; vec3 nr = getNormalFast(pr); g_cnt_off--;\n    \n\t// return simple depth texture", s)
+    return s
+
+
+HEADER = """#version 300 es
+precision highp float;
+precision highp int;
+in vec2 v_uv;
+out vec4 o_col;
+int g_evals = 0;
+int g_cnt_off = 0;
+"""
+
+
+def count_hook(s: str, sig: str) -> str:
+    """Insert the eval counter at the top of the scene's sceneSDF body."""
+    k = s.index(sig)
+    k = s.index("{", k) + 1
+    return s[:k] + "\n\tif (g_cnt_off == 0) g_evals++;" + s[k:]
+
+
+def main_rewrite(s: str) -> str:
+    s = s.replace("gl_TexCoord[0].xy", "v_uv")
+    head, sep, tail = s.rpartition("col = vignette(col, v_uv);")
+    if not sep:
+        raise RuntimeError("vignette call not found")
+    s = head + "col = vignette(col, v_uv, 0.1);" + tail
+    # only the live main() (the last one; common.frag:1124-1188 holds commented-out ones)
+    head, sep, tail = s.rpartition("gl_FragColor = vec4(col, 1.0);")
+    if not sep:
+        raise RuntimeError("main() output not found")
+    return (head + "#ifdef COUNT_MODE\n\to_col = vec4(float(g_evals), 0.0, 0.0, 1.0);\n#else\n"
+            "\to_col = vec4(col, 1.0);\n#endif" + tail)
+
+
+def scene_O(ref: str) -> str:
+    s = preprocess(os.path.join(ref, "output_shader.frag"), ref)
+    s = es3_rewrite(s)
+    s = must_sub("vec3(180, u_time * 2, 0)", "vec3(180, u_time * 2.0, 0)", s)
+    s = must_sub("sd.mat.transparency > 0 ?", "sd.mat.transparency > 0.0 ?", s)
+    s = must_sub("if (sd.mat.reflectivity > 0)", "if (sd.mat.reflectivity > 0.0)", s)
+    s = must_sub("if (sd.mat.transparency > 0)", "if (sd.mat.transparency > 0.0)", s)
+    s = must_sub("float reflectivity = 0.0)", "float reflectivity)", s)  # output_shader.frag:246
+    s = count_hook(s, "SdResult sceneSDF(vec3 p)\n{")
+    return HEADER + main_rewrite(s)
+
+
+def scene_T(ref: str) -> str:
+    """template.frag repaired as SURVEY Appendix A defines scene T."""
+    with open(os.path.join(ref, "template.frag")) as f:
+        lines = f.read().split("\n")
+    # delete template.frag:3-20 (re-definitions of Material / blendMaterial)
+    body = "\n".join(lines[:2] + lines[20:])
+    body = must_sub("32.0, 0.0);", "32.0, 0.0, 0.0, vec3(0), 1.0, vec3(0));", body)
+    body = must_sub("64., 0.9);", "64., 0.9, 0.0, vec3(0), 1.0, vec3(0));", body)
+    body = must_sub("128.0, 0.0);", "128.0, 0.0, 0.0, vec3(0), 1.0, vec3(0));", body)
+    body = must_sub("return dist;", "return SdResult(dist, red);", body)
+    tmp = "#define ALLOW_MATERIAL_BLENDING\n" + body
+    s = _preprocess_text(tmp, ref)
+    s = es3_rewrite(s)
+    s = must_sub("vec3(180, u_time * 2, 0)", "vec3(180, u_time * 2.0, 0)", s)
+    s = count_hook(s, "SdResult sceneSDF(in vec3 p)\n{")
+    return HEADER + main_rewrite(s)
+
+
+def scene_S0(ref: str) -> str:
+    """Config 1 scene (defined by this build): the reference
+    library with a one-sphere sceneSDF and a lambert render()."""
+    s = "#define ALLOW_MATERIAL_BLENDING\n#include \"common.frag\"\n" + """
+const Material red = Material(vec3(0.2, 0.02, 0.02), vec3(0.04, 0.02, 0.02), 32.0, 0.0, 0.0, vec3(0), 1.0, vec3(0));
+SdResult sceneSDF(vec3 p)
+{
+	return SdResult(sphere(vec4(0.0, 1.0, -3.0, 1.0), p), red);
+}
+vec3 background(vec3 ro, vec3 rd)
+{
+	vec3 color = vec3(0);
+	return applyScattering(color, ro, ro + rd * ZFAR, vec3(0.34, 0.435, 0.57), vec3(2.0), vec3(2.0));
+}
+vec3 render(in vec3 ro, in vec3 rd)
+{
+	SdResult sd = castRayD(ro, rd);
+	if (sd.dist > 0.0)
+	{
+		vec3 p = ro + rd * sd.dist;
+		vec3 n = getNormalFast(p);
+		vec3 lightDir = normalize(vec3(20, 50, 0) - p);
+		return sd.mat.diffuse * (0.1 + lambert(lightDir, n));
+	}
+	return background(ro, rd);
+}
+void main()
+{
+	vec2 uv = (gl_TexCoord[0].xy - 0.5) * u_resolution / u_resolution.y;
+	vec3 rayOrigin = u_pos;
+	vec3 rayDirection = normalize(vec3(uv.x, -uv.y, -1.0));
+	rayDirection.yz *= rot(-u_mouse.y);
+	rayDirection.xz *= rot(u_mouse.x);
+	vec3 col = render(rayOrigin, rayDirection);
+	col = tonemap(col);
+	col = contrast(col);
+	col = vignette(col, gl_TexCoord[0].xy);
+	gl_FragColor = vec4(col, 1.0);
+}
+"""
+    s = _preprocess_text(s, ref)
+    s = es3_rewrite(s)
+    s = count_hook(s, "SdResult sceneSDF(vec3 p)\n{")
+    return HEADER + main_rewrite(s)
+
+
+def _preprocess_text(text: str, root: str) -> str:
+    out = []
+    for line in text.split("\n"):
+        k = line.find("#include")
+        if k != -1 and (k == 0 or line.rfind("//", 0, k) == -1):
+            m = re.search(r'["<]([^">]*)[">]', line[k + 8:])
+            out.append(preprocess(os.path.join(root, m.group(1)), root))
+            continue
+        out.append(line)
+    return "\n".join(out)
+
+
+def set_max_steps(src: str, n: int) -> str:
+    if n == 128:  # the reference's own value (common.frag:15)
+        return src
+    return must_sub("const int MAX_MARCHING_STEPS = 128;", f"const int MAX_MARCHING_STEPS = {n};", src)
+
+
+# ------------------------------------------------------------- EGL / GLES3
+
+VS = """#version 300 es
+out vec2 v_uv;
+void main() {
+    vec2 p = vec2(float((gl_VertexID << 1) & 2), float(gl_VertexID & 2));
+    v_uv = vec2(p.x, 1.0 - p.y);
+    gl_Position = vec4(2.0 * p - 1.0, 0.0, 1.0);
+}
+"""
+
+
+class GL:
+    def __init__(self, W, H):
+        self.egl = egl = ctypes.CDLL(SS + "libEGL.so")
+        self.gl = gl = ctypes.CDLL(SS + "libGLESv2.so")
+        vp = ctypes.c_void_p
+        egl.eglGetDisplay.restype = vp
+        egl.eglChooseConfig.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp), ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_int)]
+        egl.eglCreatePbufferSurface.restype = vp
+        egl.eglCreatePbufferSurface.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
+        egl.eglCreateContext.restype = vp
+        egl.eglCreateContext.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_int)]
+        egl.eglMakeCurrent.argtypes = [vp, vp, vp, vp]
+        egl.eglInitialize.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        dpy = egl.eglGetDisplay(vp(0))
+        a, b = ctypes.c_int(), ctypes.c_int()
+        assert egl.eglInitialize(vp(dpy), ctypes.byref(a), ctypes.byref(b))
+        EGL_NONE = 0x3038
+        attrs = (ctypes.c_int * 15)(0x3033, 0x0001, 0x3040, 0x0040, 0x3024, 8, 0x3023, 8, 0x3022, 8, 0x3021, 8,
+                                    EGL_NONE, 0, 0)
+        cfg = vp()
+        n = ctypes.c_int()
+        assert egl.eglChooseConfig(vp(dpy), attrs, ctypes.byref(cfg), 1, ctypes.byref(n)) and n.value > 0
+        sattr = (ctypes.c_int * 5)(0x3057, W, 0x3056, H, EGL_NONE)
+        surf = egl.eglCreatePbufferSurface(vp(dpy), cfg, sattr)
+        egl.eglBindAPI(0x30A0)
+        cattr = (ctypes.c_int * 3)(0x3098, 3, EGL_NONE)
+        ctx = egl.eglCreateContext(vp(dpy), cfg, vp(0), cattr)
+        assert ctx, "eglCreateContext failed"
+        assert egl.eglMakeCurrent(vp(dpy), vp(surf), vp(surf), vp(ctx))
+        gl.glGetString.restype = ctypes.c_char_p
+        self.renderer = gl.glGetString(0x1F01).decode()
+        self.version = gl.glGetString(0x1F02).decode()
+        self.W, self.H = W, H
+        u = ctypes.c_uint()
+        gl.glGenVertexArrays(1, ctypes.byref(u))
+        gl.glBindVertexArray(u)
+        tex, fbo = ctypes.c_uint(), ctypes.c_uint()
+        gl.glGenTextures(1, ctypes.byref(tex))
+        gl.glBindTexture(0x0DE1, tex)
+        gl.glTexStorage2D(0x0DE1, 1, 0x8814, W, H)  # GL_RGBA32F
+        gl.glGenFramebuffers(1, ctypes.byref(fbo))
+        gl.glBindFramebuffer(0x8D40, fbo)
+        gl.glFramebufferTexture2D(0x8D40, 0x8CE0, 0x0DE1, tex, 0)
+        st = gl.glCheckFramebufferStatus(0x8D40)
+        assert st == 0x8CD5, hex(st)
+        gl.glViewport(0, 0, W, H)
+        gl.glGetUniformLocation.argtypes = [ctypes.c_uint, ctypes.c_char_p]
+        for fn in ("glUniform1f", "glUniform2f", "glUniform3f"):
+            getattr(gl, fn).argtypes = [ctypes.c_int] + [ctypes.c_float] * int(fn[-2])
+
+    def shader(self, kind, src):
+        gl = self.gl
+        sh = gl.glCreateShader(kind)
+        b = src.encode()
+        arr = (ctypes.c_char_p * 1)(b)
+        ln = (ctypes.c_int * 1)(len(b))
+        gl.glShaderSource(sh, 1, arr, ln)
+        gl.glCompileShader(sh)
+        ok = ctypes.c_int()
+        gl.glGetShaderiv(sh, 0x8B81, ctypes.byref(ok))
+        if not ok.value:
+            buf = ctypes.create_string_buffer(65536)
+            gl.glGetShaderInfoLog(sh, 65536, None, buf)
+            raise RuntimeError("compile failed:\n" + buf.value.decode())
+        return sh
+
+    def program(self, fs_src):
+        gl = self.gl
+        p = gl.glCreateProgram()
+        gl.glAttachShader(p, self.shader(0x8B31, VS))
+        gl.glAttachShader(p, self.shader(0x8B30, fs_src))
+        gl.glLinkProgram(p)
+        ok = ctypes.c_int()
+        gl.glGetProgramiv(p, 0x8B82, ctypes.byref(ok))
+        if not ok.value:
+            buf = ctypes.create_string_buffer(65536)
+            gl.glGetProgramInfoLog(p, 65536, None, buf)
+            raise RuntimeError("link failed:\n" + buf.value.decode())
+        return p
+
+    def draw(self, prog, pose, res):
+        gl = self.gl
+        gl.glUseProgram(prog)
+
+        def loc(n):
+            return gl.glGetUniformLocation(prog, n.encode())
+        gl.glUniform2f(loc("u_resolution"), float(res[0]), float(res[1]))
+        gl.glUniform3f(loc("u_pos"), *[float(v) for v in pose["pos"]])
+        gl.glUniform2f(loc("u_mouse"), *[float(v) for v in pose["mouse"]])
+        gl.glUniform1f(loc("u_time"), float(pose["time"]))
+        gl.glDrawArrays(0x0004, 0, 3)
+        gl.glFinish()
+        buf = np.zeros((self.H, self.W, 4), np.float32)
+        gl.glReadPixels(0, 0, self.W, self.H, 0x1908, 0x1406, buf.ctypes.data_as(ctypes.c_void_p))
+        err = gl.glGetError()
+        assert err == 0, hex(err)
+        return buf[::-1].copy()  # GL rows bottom-up -> row 0 = tc.y 0.5/H
+
+
+# ------------------------------------------------------------- fixtures
+
+FIXTURES = [
+    # name, scene, W, H, pose, max_steps
+    ("S0_64_P0", "S0", 64, 64, "S0", 64),
+    ("T_64_P0", "T", 64, 64, "P0", 128),
+    ("T_96x54_P1", "T", 96, 54, "P1", 128),
+    ("T_64_P4_256", "T", 64, 64, "P4", 256),
+    ("T_80x48_P7", "T", 80, 48, "P7", 128),
+    ("O_64_P0", "O", 64, 64, "P0", 128),
+    ("O_96x54_P2", "O", 96, 54, "P2", 128),
+    ("O_64_P6", "O", 64, 64, "P6", 128),
+    ("O_72x40_P3_512", "O", 72, 40, "P3", 512),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    builders = {"O": scene_O, "T": scene_T, "S0": scene_S0}
+    for name, scene, W, H, pose_name, steps in FIXTURES:
+        if args.only and args.only not in name:
+            continue
+        pose = S0_POSE if pose_name == "S0" else POSES[pose_name]
+        src = set_max_steps(builders[scene](args.ref), steps)
+        g = GL(W, H)
+        t0 = time.time()
+        rgba = g.draw(g.program(src), pose, (W, H))
+        cnt = g.draw(g.program(src.replace("precision highp int;\n", "precision highp int;\n#define COUNT_MODE\n", 1)),
+                     pose, (W, H))
+        dt = time.time() - t0
+        meta = dict(scene=scene, W=W, H=H, pose=pose_name, pos=list(pose["pos"]), mouse=list(pose["mouse"]),
+                    time=pose["time"], max_steps=steps, renderer=g.renderer, gl_version=g.version,
+                    generator="tests/golden/make_goldens.py")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), rgba=rgba, evals=cnt[..., 0].astype(np.int32),
+                            meta=json.dumps(meta))
+        print(f"{name}: {dt:.2f}s mean={rgba[..., :3].mean():.4f} evals/px={cnt[..., 0].mean():.2f} "
+              f"nan={int(np.isnan(rgba).sum())}")
+
+
+if __name__ == "__main__":
+    main()
