@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""bench.py -- ray-steps/s and frames/s of the HIP ray-march pass on MI355X.
+
+Workload (BASELINE.json metric "ray-steps/sec + frames/sec at 4096x4096,
+1/2/4/8 MI355X"): config C3/C4 -- a 4096x4096 frame of scene T (the repaired
+template.frag: Menger sponge, castRay + reflection march + AO + soft shadow),
+256 max steps, reference start pose P0.  One step = one frame: every rank
+renders its row bands (rows dealt in bands of 16, round robin), packs them to
+RGBA8 (the reference's RenderTexture format), and for N > 1 one RCCL gather
+brings them to rank 0, which de-interleaves the frame.  Total work per step is
+fixed as N grows (strong scaling).  The inputs are uniforms only (synthetic:
+the pose), nothing is read from the host inside the timed region.
+
+value = sceneSDF evaluations (ray-steps) of one frame x steps / wall time of
+the timed region (max over ranks).  The per-frame step count comes from one
+instrumented run of the same kernel (count_evals) before timing; the timed
+runs are uninstrumented.
+
+Usage: python bench.py [--gpus N --steps K --warmup W] [--scene T|O|S0]
+       [--size 4096] [--max-steps 256] [--pose P0] [--band 16]
+       [--fmt rgba8|float4] [--kernel auto|direct|wave] [--cpu-seconds 12]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector, /opt/skills/guides/MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0     # HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scene", default="T")
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--max-steps", type=int, default=256)
+    ap.add_argument("--pose", default="P0")
+    ap.add_argument("--band", type=int, default=16)
+    ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "wave"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--pmc", default=os.path.join(HERE, "profiles", "pmc_traffic.json"),
+                    help="rocprofv3 PMC summary used for roofline.traffic (if it matches the workload)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, pose, W, H, target_s):
+    """Oracle (CPU restatement, -O3 build) on a strided row sample of the same frame."""
+    import oracle  # test infrastructure: only the cpu_baseline leg uses it
+    import numpy as np
+
+    L = oracle.lib(fast=True)
+    kw = dict(pos=pose["pos"], mouse=pose["mouse"], time=pose["time"], max_steps=args.max_steps)
+    # calibrate on 8 evenly spread rows, then size the sample to ~target_s
+    probe = np.linspace(0, H - 1, 8).astype(np.int32)
+    t0 = time.perf_counter()
+    oracle.render_rows(args.scene, W, H, probe, fast=True, **kw)
+    per_row = (time.perf_counter() - t0) / len(probe)
+    nrows = int(max(8, min(H, target_s / max(per_row, 1e-6))))
+    stride = max(1, H // nrows)
+    rows = np.arange(0, H, stride, dtype=np.int32)
+    t0 = time.perf_counter()
+    _, ev = oracle.render_rows(args.scene, W, H, rows, fast=True, **kw)
+    dt = time.perf_counter() - t0
+    evals = int(ev.sum(dtype=np.uint64))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": evals / dt,
+        "unit": "ray-steps/s",
+        "frames_per_s": (len(rows) / H) / dt,
+        "cores": int(L.oracle_num_threads()),
+        "kind": "port",
+        "sample": f"rows y = 0 mod {stride} of the {W}x{H} frame ({len(rows)} rows, {evals} ray-steps, "
+                  f"{dt:.2f} s); frames/s extrapolated by row fraction; OpenMP dynamic rows, -O3 "
+                  f"x86-64-v3; host CPU: {model}, nproc={os.cpu_count()}",
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import raymarching_amd as rm
+    from raymarching_amd.frame import DistributedFrame
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W = args.size
+    H = args.height or args.size
+    pose = rm.S0_POSE if args.scene == "S0" else rm.POSES[args.pose]
+    r = rm.Renderer(local)
+    r.load_scene(rm.SCENE_FILES[args.scene])
+    r.set_uniform("u_resolution", W, H)
+    r.set_pose(pose["pos"], pose["mouse"], pose["time"])
+    r.set_params(max_steps=args.max_steps, shadow_max_steps=0, kernel=args.kernel)
+    stream = torch.cuda.current_stream(dev)
+    r.set_stream(stream)
+    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt)
+
+    # instrumented run: ray-steps of this rank's rows, summed over ranks
+    r.set_params(count_evals=1)
+    _, st = fr.render_local(stats=True)
+    r.set_params(count_evals=0)
+    ev_rank = torch.tensor([st["evals"]], dtype=torch.float64, device=dev)
+    ev_total = ev_rank.clone()
+    if world > 1:
+        dist.all_reduce(ev_total)
+    evals_rank, evals_frame = int(ev_rank.item()), int(ev_total.item())
+
+    for _ in range(args.warmup):
+        fr.render()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    k0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    k1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        k0[i].record(stream)
+        fr.render_local()
+        k1[i].record(stream)
+        fr.finish()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    kern = sum(a.elapsed_time(b) for a, b in zip(k0, k1)) / args.steps  # ms, this rank
+    kt = torch.tensor([kern], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+    elapsed, kern_max = float(t.item()), float(kt.item())
+
+    if rank == 0:
+        F = rm.FLOP_PER_EVAL[args.scene]
+        ach = evals_rank * F / (kern / 1e3) / 1e12
+        out_bytes = W * fr.plan.count(0) * 16
+        traffic = None
+        try:
+            pm = json.load(open(args.pmc))
+            key = f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}"
+            traffic = pm.get(key, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        res = {
+            "metric": "ray-steps/sec + frames/sec at 4096\u00d74096, 1/2/4/8 MI355X",
+            "value": evals_frame * args.steps / elapsed,
+            "unit": "ray-steps/s",
+            "frames_per_s": args.steps / elapsed,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: uniforms only (camera pose), no input data",
+            "config": {
+                "workload": f"C{3 if world == 1 else 4}: {W}x{H} scene {args.scene} "
+                            f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
+                            f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0",
+                "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
+                "band": args.band, "fmt": args.fmt, "kernel": args.kernel,
+                "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
+            },
+            "kernel_ms": kern, "kernel_ms_max_rank": kern_max,
+            "roofline": {
+                "bound": "valu", "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic,
+                "flop_per_ray_step": F, "ray_steps_per_launch": evals_rank,
+                "hbm": {"achieved": out_bytes / (kern / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": out_bytes / (kern / 1e3) / 1e9 / PEAK_HBM_GBS,
+                        "algorithmic_bytes_per_launch": out_bytes},
+            },
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            res["cpu_baseline"] = cpu_baseline(args, pose, W, H, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

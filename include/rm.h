@@ -1,0 +1,133 @@
+/*
+ * rm.h -- C ABI of librm.so, the MI355X (gfx950) ray-march pass.
+ *
+ * Drop-in boundary for the reference's full-screen fragment pass
+ * (cahekp/Raymarching).  The reference drives that pass through SFML:
+ *
+ *   ShaderLoader::loadFromFile(file, sf::Shader::Fragment, shader)
+ *       source/shader_loader.h:11, source/shader_loader.cpp:8-20
+ *   shader.setUniform("u_resolution" | "u_pos" | "u_mouse" | "u_time" | ...)
+ *       main.cpp:54,187-194 (include/SFML/Graphics/Shader.hpp:297,306,315)
+ *   renderTexture.draw(fullScreenSprite, &shader)
+ *       main.cpp:199,205 (include/SFML/Graphics/RenderTarget.hpp:237)
+ *
+ * and each entry point below replaces one of those calls (see the per-call
+ * comments and INTEGRATION.md).  Conventions: every call returns an
+ * rm_status (no exceptions cross the ABI); buffers are caller-owned; one
+ * rm_ctx per host thread; uniforms/params are state of the ctx, read at the
+ * next render call, as GL uniforms are read at the next draw.
+ *
+ * Pixel convention: out[row*W + col] is the fragment with
+ * gl_TexCoord = ((col+0.5)/W, (row+0.5)/H); row 0 is first in memory and
+ * looks up.  Pixels are RGBA float32 (gl_FragColor,
+ * alpha = 1) or, from the *_rgba8 calls, RGBA8 unorm as the reference's
+ * sf::RenderTexture stores them.
+ */
+#ifndef RM_H_
+#define RM_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum rm_status {
+    RM_OK = 0,
+    RM_ERR_INVALID_ARGUMENT = 1, /* bad pointer/size/uniform arity                       */
+    RM_ERR_FILE = 2,             /* "can't load file" (source/shader_loader.cpp:26-30)  */
+    RM_ERR_SCENE = 3,            /* no scene plugin for this source (cf. GL compile fail) */
+    RM_ERR_NO_SCENE = 4,         /* render before a successful rm_load_scene            */
+    RM_ERR_DEVICE = 5,           /* HIP runtime error (message in rm_last_error)        */
+    RM_ERR_OUT_OF_MEMORY = 6
+} rm_status;
+
+typedef struct rm_ctx rm_ctx;
+
+/* Run-time knobs that replace the reference's compile-time constants. */
+typedef struct rm_params {
+    int32_t max_steps;        /* MAX_MARCHING_STEPS, common.frag:15 (default 128)        */
+    int32_t shadow_max_steps; /* softshadow2 cap; 0 = unbounded as common.frag:814       */
+    int32_t count_evals;      /* 1: instrumented kernel, rm_stats.evals = sceneSDF calls */
+    int32_t kernel;           /* 0 = auto, 1 = direct (lane per pixel), 2 = wave state machine */
+} rm_params;
+
+typedef struct rm_stats {
+    uint64_t evals;  /* sceneSDF calls (ray-steps) of this render, when count_evals   */
+    uint64_t pixels; /* pixels rendered                                                */
+    float kernel_ms; /* device time of the render kernel (HIP events on the ctx stream) */
+    int32_t scene;   /* scene id that ran                                              */
+} rm_stats;
+
+/* Create a context on HIP device `device`.  Scene unset, params default. */
+rm_status rm_create(rm_ctx **out, int device);
+rm_status rm_destroy(rm_ctx *ctx);
+
+/* Replaces ShaderLoader::loadFromFile (source/shader_loader.cpp:8-20).
+ * If `file_name` exists it is preprocessed with the reference's #include
+ * semantics (source/shader_loader.cpp:22-81; missing include -> RM_ERR_FILE).
+ * The scene plugin is chosen by the file's base name: "output_shader.frag"
+ * (scene O), "template.frag" (scene T, repaired as SURVEY.md App. A),
+ * "sphere" (scene S0), "output_shader_glass" (test scene OG).  A registered
+ * name needs no file on disk (the GPU host has no shader tree).  Unknown name
+ * and no file -> RM_ERR_FILE; unknown name with a file -> RM_ERR_SCENE. */
+rm_status rm_load_scene(rm_ctx *ctx, const char *file_name);
+
+/* Replace sf::Shader::setUniform (include/SFML/Graphics/Shader.hpp:297,306,315)
+ * for the names main.cpp sets: u_resolution (2f), u_pos (3f), u_mouse (2f),
+ * u_time (1f), u_sample_part (1f), u_seed1/u_seed2 (2f).  The last three are
+ * declared but unused by the scenes (common.frag:8-11) and are accepted and
+ * ignored; other names warn once on stderr and are ignored, as SFML does for
+ * uniforms the GLSL compiler removed.  Wrong arity -> RM_ERR_INVALID_ARGUMENT. */
+rm_status rm_set_uniform1f(rm_ctx *ctx, const char *name, float x);
+rm_status rm_set_uniform2f(rm_ctx *ctx, const char *name, float x, float y);
+rm_status rm_set_uniform3f(rm_ctx *ctx, const char *name, float x, float y, float z);
+
+rm_status rm_set_params(rm_ctx *ctx, const rm_params *params);
+rm_status rm_get_params(rm_ctx *ctx, rm_params *params);
+
+/* Stream the ctx launches on (a hipStream_t; NULL = the null stream). */
+rm_status rm_set_stream(rm_ctx *ctx, void *hip_stream);
+rm_status rm_synchronize(rm_ctx *ctx);
+
+/* Replaces renderTexture.draw(sprite, &shader) (main.cpp:199,205): run the
+ * pass over a W x H target into `out` (W*H*4 float).  Device `out`: the call
+ * is asynchronous on the ctx stream unless `stats` is non-NULL (then it
+ * waits and fills stats).  Host `out`: rendered through a device staging
+ * buffer and copied back before returning. */
+rm_status rm_render(rm_ctx *ctx, int W, int H, float *out, rm_stats *stats);
+
+/* Same pass over one shard of a W x H frame: frame row y belongs to shard
+ * (y / band) % nshards; the shard's rows are packed into `out` in increasing
+ * y (rm_shard_rows() rows of W float4).  Used by row-sharded multi-GPU frames. */
+rm_status rm_render_band(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out,
+                         rm_stats *stats);
+
+/* Number of frame rows shard `shard` owns. */
+rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows);
+
+/* Root side of a row-sharded frame: `gathered` holds nshards consecutive
+ * blocks of rows_per_shard packed rows (rows_per_shard >= every shard's row
+ * count); writes the W x H frame into `out`.  Device pointers, ctx stream. */
+rm_status rm_deinterleave(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
+                          const float *gathered, float *out);
+
+/* rm_deinterleave for RGBA8 frames (uint32 per pixel). */
+rm_status rm_deinterleave_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
+                                const uint32_t *gathered, uint32_t *out);
+
+/* float RGBA -> RGBA8 unorm (round to nearest, clamped), device pointers. */
+rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t *out);
+
+/* rm_render + rm_pack_rgba8 into a W*H uint32 target (device or host). */
+rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats);
+
+/* Message of the last failing call on ctx ("" if none). */
+const char *rm_last_error(rm_ctx *ctx);
+const char *rm_status_string(rm_status status);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RM_H_ */

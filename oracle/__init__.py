@@ -74,6 +74,8 @@ def lib(fast: bool = False) -> ctypes.CDLL:
                       ("oracle_smin_cubic", 3), ("oracle_hash11", 1)):
             getattr(L, fn).argtypes = [ctypes.c_float] * n
             getattr(L, fn).restype = ctypes.c_float
+        L.oracle_num_threads.argtypes = []
+        L.oracle_num_threads.restype = ctypes.c_int
         _LIBS[name] = L
     return _LIBS[name]
 

@@ -22,6 +22,7 @@
  * Every function cites the reference file:line it restates.
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -754,6 +755,9 @@ int oracle_normal(int scene, const oracle_uniforms *u, const float *pts, int n, 
     }
     return 0;
 }
+
+/* OpenMP threads a render uses (reported as the CPU baseline's core count). */
+int oracle_num_threads(void) { return omp_get_max_threads(); }
 
 /* Built-in KATs: name -> f(x, y, z) */
 float oracle_glsl_mod(float x, float y) { return gmod(x, y); }

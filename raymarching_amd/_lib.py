@@ -1,0 +1,98 @@
+"""ctypes binding of librm.so (include/rm.h).
+
+The product path has no CPU fallback: if librm.so is missing or fails to
+load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+# RM_LIB may point at an alternative in-tree build (experiments); default librm.so
+LIB_PATH = os.environ.get("RM_LIB") or os.path.join(HERE, "librm.so")
+
+RM_OK = 0
+STATUS = {0: "RM_OK", 1: "RM_ERR_INVALID_ARGUMENT", 2: "RM_ERR_FILE", 3: "RM_ERR_SCENE",
+          4: "RM_ERR_NO_SCENE", 5: "RM_ERR_DEVICE", 6: "RM_ERR_OUT_OF_MEMORY"}
+
+# every symbol include/rm.h declares
+EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_set_uniform2f",
+           "rm_set_uniform3f", "rm_set_params", "rm_get_params", "rm_set_stream", "rm_synchronize",
+           "rm_render", "rm_render_band", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8", "rm_pack_rgba8",
+           "rm_render_rgba8", "rm_last_error", "rm_status_string")
+
+
+class RmParams(ctypes.Structure):
+    _fields_ = [("max_steps", ctypes.c_int32), ("shadow_max_steps", ctypes.c_int32),
+                ("count_evals", ctypes.c_int32), ("kernel", ctypes.c_int32)]
+
+
+class RmStats(ctypes.Structure):
+    _fields_ = [("evals", ctypes.c_uint64), ("pixels", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
+                ("scene", ctypes.c_int32)]
+
+    def as_dict(self):
+        return dict(evals=int(self.evals), pixels=int(self.pixels), kernel_ms=float(self.kernel_ms),
+                    scene=int(self.scene))
+
+
+class RmError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"{STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load librm.so (raises if it is missing: no fallback path exists)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built; run `make -C raymarching_amd` (or __graft_entry__.build())")
+    # torch ships its own libamdhip64.so.7: load it first so that librm.so binds
+    # to the same HIP runtime (one runtime per process; tensors and streams
+    # are then shared).  A process without torch uses /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401,PLC0415
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, c = ctypes.c_void_p, ctypes
+    cp = c.c_char_p
+    sig = {
+        "rm_create": ([c.POINTER(vp), c.c_int], c.c_int),
+        "rm_destroy": ([vp], c.c_int),
+        "rm_load_scene": ([vp, cp], c.c_int),
+        "rm_set_uniform1f": ([vp, cp, c.c_float], c.c_int),
+        "rm_set_uniform2f": ([vp, cp, c.c_float, c.c_float], c.c_int),
+        "rm_set_uniform3f": ([vp, cp, c.c_float, c.c_float, c.c_float], c.c_int),
+        "rm_set_params": ([vp, c.POINTER(RmParams)], c.c_int),
+        "rm_get_params": ([vp, c.POINTER(RmParams)], c.c_int),
+        "rm_set_stream": ([vp, vp], c.c_int),
+        "rm_synchronize": ([vp], c.c_int),
+        "rm_render": ([vp, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
+        "rm_render_band": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
+        "rm_shard_rows": ([c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_int)], c.c_int),
+        "rm_deinterleave": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp], c.c_int),
+        "rm_deinterleave_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp], c.c_int),
+        "rm_pack_rgba8": ([vp, c.c_int64, vp, vp], c.c_int),
+        "rm_render_rgba8": ([vp, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
+        "rm_last_error": ([vp], cp),
+        "rm_status_string": ([c.c_int], cp),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _LIB = L
+    return L
+
+
+def check(status: int, ctx=None) -> None:
+    if status != RM_OK:
+        msg = lib().rm_last_error(ctx).decode() if ctx else ""
+        raise RmError(status, msg)

@@ -1,0 +1,228 @@
+"""Host-side mirror of the reference's shader-pass surface, over librm.so.
+
+The reference drives its ray-march pass through SFML (main.cpp:52-54,187-207):
+
+    sf::Shader shader;
+    ShaderLoader::loadFromFile("output_shader.frag", sf::Shader::Fragment, shader);
+    shader.setUniform("u_resolution", sf::Vector2f(wf, hf));
+    ...
+    shader.setUniform("u_pos", pos); shader.setUniform("u_mouse", ...);
+    shader.setUniform("u_time", t);
+    outputTexture.draw(firstTextureSpriteFlipped, &shader);
+
+The same names, argument meaning and error behaviour exist here:
+``ShaderLoader.loadFromFile(file, Shader.Fragment, shader) -> bool`` (prints
+and returns False on failure, source/shader_loader.cpp:26-30),
+``Shader.setUniform(name, value)`` and ``RenderTexture.draw(shader)``, whose
+target is a W x H x 4 float32 tensor resident in HBM.  ``Renderer`` is the
+lower-level handle (one librm context) used by bench.py and the tests.
+"""
+from __future__ import annotations
+
+import ctypes
+import sys
+
+from . import _lib
+from ._lib import RmParams, RmStats, check, lib
+
+
+def _torch():
+    import torch  # noqa: PLC0415  (torch provides device memory and streams only)
+    return torch
+
+
+class Renderer:
+    """One librm context on one HIP device."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        self._ctx = ctypes.c_void_p()
+        st = L.rm_create(ctypes.byref(self._ctx), int(device))
+        if st != 0:
+            raise _lib.RmError(st, f"rm_create(device={device}) failed")
+        self.device = int(device)
+
+    def close(self):
+        if self._ctx:
+            lib().rm_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    # --- state ---------------------------------------------------------
+    def load_scene(self, name: str) -> None:
+        check(lib().rm_load_scene(self._ctx, name.encode()), self._ctx)
+
+    def set_uniform(self, name: str, *v: float) -> None:
+        L = lib()
+        n = name.encode()
+        if len(v) == 1:
+            st = L.rm_set_uniform1f(self._ctx, n, float(v[0]))
+        elif len(v) == 2:
+            st = L.rm_set_uniform2f(self._ctx, n, float(v[0]), float(v[1]))
+        elif len(v) == 3:
+            st = L.rm_set_uniform3f(self._ctx, n, float(v[0]), float(v[1]), float(v[2]))
+        else:
+            raise ValueError("uniforms have 1..3 float components")
+        check(st, self._ctx)
+
+    def set_pose(self, pos, mouse, time) -> None:
+        self.set_uniform("u_pos", *pos)
+        self.set_uniform("u_mouse", *mouse)
+        self.set_uniform("u_time", time)
+
+    def set_params(self, max_steps=None, shadow_max_steps=None, count_evals=None, kernel=None) -> None:
+        p = self.params()
+        if max_steps is not None:
+            p.max_steps = int(max_steps)
+        if shadow_max_steps is not None:
+            p.shadow_max_steps = int(shadow_max_steps)
+        if count_evals is not None:
+            p.count_evals = int(bool(count_evals))
+        if kernel is not None:
+            p.kernel = {"auto": 0, "direct": 1, "wave": 2}.get(kernel, kernel)
+        check(lib().rm_set_params(self._ctx, ctypes.byref(p)), self._ctx)
+
+    def params(self) -> RmParams:
+        p = RmParams()
+        check(lib().rm_get_params(self._ctx, ctypes.byref(p)), self._ctx)
+        return p
+
+    def set_stream(self, stream) -> None:
+        """stream: a torch.cuda.Stream, a raw hipStream_t int, or None."""
+        raw = getattr(stream, "cuda_stream", stream)
+        check(lib().rm_set_stream(self._ctx, ctypes.c_void_p(raw or 0)), self._ctx)
+
+    def synchronize(self) -> None:
+        check(lib().rm_synchronize(self._ctx), self._ctx)
+
+    # --- passes ----------------------------------------------------------
+    @staticmethod
+    def _ptr(t):
+        return ctypes.c_void_p(t.data_ptr()) if hasattr(t, "data_ptr") else ctypes.c_void_p(t.ctypes.data)
+
+    def render(self, W: int, H: int, out=None, stats: bool = False):
+        """Full frame into `out` (device tensor [H,W,4] f32; allocated if None)."""
+        torch = _torch()
+        if out is None:
+            out = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{self.device}")
+        _check_out(out, H * W * 4)
+        s = RmStats()
+        check(lib().rm_render(self._ctx, int(W), int(H), self._ptr(out), ctypes.byref(s) if stats else None),
+              self._ctx)
+        return (out, s.as_dict()) if stats else out
+
+    def render_band(self, W: int, H: int, band: int, nshards: int, shard: int, out=None, stats: bool = False):
+        """Rows y with (y // band) % nshards == shard, packed in increasing y."""
+        torch = _torch()
+        n = shard_rows(H, band, nshards, shard)
+        if out is None:
+            out = torch.empty((n, W, 4), dtype=torch.float32, device=f"cuda:{self.device}")
+        _check_out(out, n * W * 4)
+        s = RmStats()
+        check(lib().rm_render_band(self._ctx, int(W), int(H), int(band), int(nshards), int(shard), self._ptr(out),
+                                   ctypes.byref(s) if stats else None), self._ctx)
+        return (out, s.as_dict()) if stats else out
+
+    def deinterleave(self, W, H, band, nshards, rows_per_shard, gathered, out=None):
+        """gathered: [nshards, rows_per_shard, W, 4] f32 or [nshards, rows_per_shard, W] RGBA8 words."""
+        torch = _torch()
+        rgba8 = gathered.dtype != torch.float32  # RGBA8 words travel as int32
+        per_px = 1 if rgba8 else 4
+        if out is None:
+            shape = (H, W) if rgba8 else (H, W, 4)
+            out = torch.empty(shape, dtype=gathered.dtype, device=gathered.device)
+        _check_out(out, H * W * per_px)
+        _check_out(gathered, nshards * rows_per_shard * W * per_px)
+        fn = lib().rm_deinterleave_rgba8 if rgba8 else lib().rm_deinterleave
+        check(fn(self._ctx, W, H, band, nshards, rows_per_shard, self._ptr(gathered), self._ptr(out)), self._ctx)
+        return out
+
+    def pack_rgba8(self, frame, out=None):
+        torch = _torch()
+        npx = frame.numel() // 4
+        if out is None:
+            out = torch.empty(frame.shape[:-1], dtype=torch.int32, device=frame.device)
+        if out.numel() < npx or out.element_size() != 4 or not out.is_contiguous():
+            raise ValueError("pack_rgba8: out must be a contiguous 32-bit tensor with one element per pixel")
+        check(lib().rm_pack_rgba8(self._ctx, npx, self._ptr(frame), self._ptr(out)), self._ctx)
+        return out
+
+    def render_rgba8(self, W, H, out=None, stats=False):
+        torch = _torch()
+        if out is None:
+            out = torch.empty((H, W), dtype=torch.int32, device=f"cuda:{self.device}")
+        s = RmStats()
+        check(lib().rm_render_rgba8(self._ctx, W, H, self._ptr(out), ctypes.byref(s) if stats else None),
+              self._ctx)
+        return (out, s.as_dict()) if stats else out
+
+
+def _check_out(t, nfloats):
+    if not t.is_contiguous() or t.numel() < nfloats or t.element_size() != 4:
+        raise ValueError(f"buffer must be contiguous 32-bit with >= {nfloats} elements")
+
+
+def shard_rows(H: int, band: int, nshards: int, shard: int) -> int:
+    n = ctypes.c_int()
+    check(lib().rm_shard_rows(int(H), int(band), int(nshards), int(shard), ctypes.byref(n)))
+    return n.value
+
+
+# ------------------------------------------------ the reference's surface
+
+
+class Shader(Renderer):
+    """sf::Shader as main.cpp uses it: a loaded scene plus its uniforms."""
+
+    Fragment = "Fragment"
+
+    def __init__(self, device: int = 0):
+        super().__init__(device)
+        self.loaded = False
+
+    def setUniform(self, name: str, value) -> None:  # noqa: N802 (SFML name)
+        vals = tuple(value) if isinstance(value, (tuple, list)) else (value,)
+        self.set_uniform(name, *vals)
+
+
+class ShaderLoader:
+    """source/shader_loader.h:8-15."""
+
+    @staticmethod
+    def loadFromFile(file_name: str, type_, out_shader: Shader) -> bool:  # noqa: N802
+        if type_ != Shader.Fragment:
+            print(f"ShaderLoader: only fragment passes exist here (got {type_})", file=sys.stderr)
+            return False
+        try:
+            out_shader.load_scene(file_name)
+        except _lib.RmError as e:
+            print(str(e), file=sys.stderr)
+            return False
+        out_shader.loaded = True
+        return True
+
+
+class RenderTexture:
+    """sf::RenderTexture stand-in: a W x H float4 target resident in HBM."""
+
+    def __init__(self):
+        self.texture = None
+
+    def create(self, W: int, H: int, device: int = 0) -> bool:
+        torch = _torch()
+        self.W, self.H = int(W), int(H)
+        self.texture = torch.zeros((H, W, 4), dtype=torch.float32, device=f"cuda:{device}")
+        return True
+
+    def draw(self, shader: Shader, stats: bool = False):
+        """Run `shader`'s pass over the whole target (main.cpp:199,205)."""
+        r = shader.render(self.W, self.H, out=self.texture, stats=stats)
+        return r[1] if stats else None
+
+    def getTexture(self):  # noqa: N802
+        return self.texture

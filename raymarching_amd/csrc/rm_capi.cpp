@@ -1,0 +1,431 @@
+// rm_capi.cpp -- the C ABI declared in include/rm.h.
+//
+// Owns the per-context state the reference keeps inside sf::Shader (uniform
+// values, the loaded scene) and turns it into the per-frame constant block the
+// kernels read (rm_device.h FrameConst).  Compiled with -ffp-contract=off so
+// that the host-side per-frame constants (sin/cos of the camera and sponge
+// rotations, the Hash11 table) are computed with the same roundings as the
+// GLSL expressions they hoist.
+#include "../../include/rm.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <set>
+#include <string>
+
+#include "rm_launch.h"
+
+using rm::FrameConst;
+
+struct rm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int scene = -1;
+    std::string scene_file;
+    // uniforms (common.frag:4-11)
+    float res[2] = {0.0f, 0.0f};
+    bool res_set = false;
+    float pos[3] = {0.0f, 0.0f, 0.0f};
+    float mouse[2] = {0.0f, 0.0f};
+    float time = 0.0f;
+    rm_params params = {128, 0, 0, 0};
+    std::string err;
+    std::set<std::string> warned;
+    unsigned long long *d_evals = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float4 *staging = nullptr;
+    size_t staging_bytes = 0;
+};
+
+namespace {
+
+rm_status fail(rm_ctx *c, rm_status s, const std::string &msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+rm_status hip_fail(rm_ctx *c, hipError_t e, const char *what) {
+    return fail(c, e == hipErrorOutOfMemory ? RM_ERR_OUT_OF_MEMORY : RM_ERR_DEVICE,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define RM_HIP(call)                                          \
+    do {                                                      \
+        hipError_t e_ = (call);                               \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+    } while (0)
+
+// ShaderLoader::preprocess (source/shader_loader.cpp:22-81): read the file
+// line by line; a line holding "#include" not preceded by "//" pulls in the
+// file named between "" or <> (path relative to the process CWD, no include
+// guards).  Returns false with the reference's message on a missing file.
+bool preprocess(const std::string &file, std::string &out, std::string &err, int depth = 0) {
+    if (depth > 64) {
+        err = "ShaderLoader: #include nesting too deep at \"" + file + "\"";
+        return false;
+    }
+    std::ifstream f(file);
+    if (!f.is_open()) {
+        err = "ShaderLoader: can't load file \"" + file + "\"";
+        return false;
+    }
+    std::string line;
+    while (std::getline(f, line)) {
+        size_t found = line.find("#include");
+        if (found != std::string::npos && (found == 0 || line.rfind("//", found) == std::string::npos)) {
+            std::string name;
+            bool reading = false;
+            for (size_t i = found + 8; i < line.size(); i++) {
+                char ch = line[i];
+                if (ch == '"' || ch == '<') reading = true;
+                else if (reading) {
+                    if (ch == '"' || ch == '>') reading = false;
+                    else name += ch;
+                }
+            }
+            if (!preprocess(name, out, err, depth + 1)) return false;
+            continue;
+        }
+        out += line + '\n';
+    }
+    return true;
+}
+
+std::string base_name(const std::string &p) {
+    size_t k = p.find_last_of("/\\");
+    return k == std::string::npos ? p : p.substr(k + 1);
+}
+
+int scene_of(const std::string &name) {
+    if (name == "output_shader.frag" || name == "O") return rm::SCENE_O;
+    if (name == "template.frag" || name == "T") return rm::SCENE_T;
+    if (name == "sphere" || name == "sphere.frag" || name == "S0") return rm::SCENE_S0;
+    if (name == "output_shader_glass" || name == "output_shader_glass.frag" || name == "OG") return rm::SCENE_OG;
+    return -1;
+}
+
+inline float fract(float x) { return x - std::floor(x); }
+
+// output_shader.frag:54-59
+float hash11(float p) {
+    float a = fract(p * 443.897f);
+    float x = a, y = a, z = a;
+    float dd = x * (y + 19.19f) + y * (z + 19.19f) + z * (x + 19.19f);
+    x += dd; y += dd; z += dd;
+    return fract((x + y) * z);
+}
+
+bool is_device_ptr(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int shard, int nrows) {
+    FrameConst F;
+    std::memset(&F, 0, sizeof(F));
+    F.res_x = c->res_set ? c->res[0] : (float)W;
+    F.res_y = c->res_set ? c->res[1] : (float)H;
+    F.pos_x = c->pos[0]; F.pos_y = c->pos[1]; F.pos_z = c->pos[2];
+    // rot(a) = mat2(cos a, -sin a, sin a, cos a) (common.frag:1088-1092)
+    float a1 = -c->mouse[1], a2 = c->mouse[0];
+    F.cam1_c = std::cos(a1); F.cam1_s = std::sin(a1);
+    F.cam2_c = std::cos(a2); F.cam2_s = std::sin(a2);
+    // transformR(.., vec3(180, u_time * 2, 0)): rotationY(-rot.y), rotationX(-rot.x)
+    // with radians(x) = x * pi/180 (common.frag:190-214,434-441)
+    float rot_y = c->time * 2.0f, rot_x = 180.0f;
+    float ay = -rot_y * 0.017453292519943295f, ax = -rot_x * 0.017453292519943295f;
+    F.ry_c = std::cos(ay); F.ry_s = std::sin(ay);
+    F.rx_c = std::cos(ax); F.rx_s = std::sin(ax);
+    F.W = W; F.H = H;
+    F.band = band; F.nshards = nshards; F.shard = shard; F.nrows = nrows;
+    F.max_steps = c->params.max_steps;
+    F.shadow_max_steps = c->params.shadow_max_steps;
+    for (int i = 0; i < 32; i++) F.hash11[i] = hash11((float)i);
+    return F;
+}
+
+int rows_of_shard(int H, int band, int nshards, int shard) {
+    int nbands = (H + band - 1) / band;
+    int n = 0;
+    // bands shard, shard + nshards, ...; the last band may be short
+    for (int b = shard; b < nbands; b += nshards) n += (b == nbands - 1) ? H - b * band : band;
+    return n;
+}
+
+rm_status ensure_staging(rm_ctx *ctx, size_t bytes) {
+    if (ctx->staging_bytes >= bytes) return RM_OK;
+    if (ctx->staging) (void)hipFree(ctx->staging);
+    ctx->staging = nullptr;
+    ctx->staging_bytes = 0;
+    RM_HIP(hipMalloc(&ctx->staging, bytes));
+    ctx->staging_bytes = bytes;
+    return RM_OK;
+}
+
+int pick_kernel(const rm_ctx *c) {
+    if (c->params.kernel == 1) return rm::KERNEL_DIRECT;
+    if (c->params.kernel == 2) return rm::KERNEL_WAVE;
+    return rm::has_wave_kernel_host(c->scene) ? rm::KERNEL_WAVE : rm::KERNEL_DIRECT;
+}
+
+// the pass itself: device output, optional stats (synchronous when given)
+rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float4 *out, rm_stats *stats) {
+    if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
+    int nrows = rows_of_shard(H, band, nshards, shard);
+    FrameConst F = frame_const(ctx, W, H, band, nshards, shard, nrows);
+    bool count = ctx->params.count_evals != 0;
+    if (count) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, sizeof(unsigned long long), ctx->stream));
+    if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+    hipError_t e = rm::launch_render(ctx->scene, F, out, count ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
+    if (stats) {
+        RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        RM_HIP(hipEventSynchronize(ctx->ev1));
+        float ms = 0.0f;
+        RM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        unsigned long long ev = 0;
+        if (count) RM_HIP(hipMemcpy(&ev, ctx->d_evals, sizeof(ev), hipMemcpyDeviceToHost));
+        stats->evals = ev;
+        stats->pixels = (uint64_t)W * (uint64_t)nrows;
+        stats->kernel_ms = ms;
+        stats->scene = ctx->scene;
+    }
+    return RM_OK;
+}
+
+rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out, rm_stats *stats) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!out || W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard/pointer");
+    if ((long long)W * H > (1LL << 31)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: frame too large");
+    RM_HIP(hipSetDevice(ctx->device));
+    if (is_device_ptr(out)) return render_dev(ctx, W, H, band, nshards, shard, reinterpret_cast<float4 *>(out), stats);
+    size_t bytes = (size_t)W * rows_of_shard(H, band, nshards, shard) * sizeof(float4);
+    rm_status s = ensure_staging(ctx, bytes);
+    if (s != RM_OK) return s;
+    s = render_dev(ctx, W, H, band, nshards, shard, ctx->staging, stats);
+    if (s != RM_OK) return s;
+    RM_HIP(hipMemcpyAsync(out, ctx->staging, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    RM_HIP(hipStreamSynchronize(ctx->stream));
+    return RM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rm_status rm_create(rm_ctx **out, int device) {
+    if (!out) return RM_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        (void)hipGetLastError();
+        return RM_ERR_DEVICE;
+    }
+    rm_ctx *ctx = new rm_ctx();
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_evals, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+    if (e != hipSuccess) {
+        rm_destroy(ctx);
+        return e == hipErrorOutOfMemory ? RM_ERR_OUT_OF_MEMORY : RM_ERR_DEVICE;
+    }
+    *out = ctx;
+    return RM_OK;
+}
+
+rm_status rm_destroy(rm_ctx *ctx) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->d_evals) (void)hipFree(ctx->d_evals);
+    if (ctx->staging) (void)hipFree(ctx->staging);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    delete ctx;
+    return RM_OK;
+}
+
+rm_status rm_load_scene(rm_ctx *ctx, const char *file_name) {
+    if (!ctx || !file_name) return RM_ERR_INVALID_ARGUMENT;
+    std::string file(file_name);
+    int sc = scene_of(base_name(file));
+    std::ifstream probe(file);
+    bool exists = probe.is_open();
+    probe.close();
+    if (exists) {
+        std::string src, err;
+        if (!preprocess(file, src, err)) {
+            std::fprintf(stderr, "%s\n", err.c_str());
+            return fail(ctx, RM_ERR_FILE, err);
+        }
+        if (sc < 0) return fail(ctx, RM_ERR_SCENE, "no HIP scene plugin for \"" + file + "\"");
+    } else if (sc < 0) {
+        std::string err = "ShaderLoader: can't load file \"" + file + "\"";
+        std::fprintf(stderr, "%s\n", err.c_str());
+        return fail(ctx, RM_ERR_FILE, err);
+    }
+    ctx->scene = sc;
+    ctx->scene_file = file;
+    ctx->err.clear();
+    return RM_OK;
+}
+
+static rm_status set_uniform(rm_ctx *ctx, const char *name, int n, float x, float y, float z) {
+    if (!ctx || !name) return RM_ERR_INVALID_ARGUMENT;
+    std::string nm(name);
+    struct U { const char *name; int n; };
+    static const U known[] = {{"u_resolution", 2}, {"u_pos", 3}, {"u_mouse", 2}, {"u_time", 1},
+                              {"u_sample_part", 1}, {"u_seed1", 2}, {"u_seed2", 2}};
+    for (const U &u : known) {
+        if (nm != u.name) continue;
+        if (n != u.n) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "uniform \"" + nm + "\" has " + std::to_string(u.n) +
+                                                                    " components, got " + std::to_string(n));
+        if (nm == "u_resolution") { ctx->res[0] = x; ctx->res[1] = y; ctx->res_set = true; }
+        else if (nm == "u_pos") { ctx->pos[0] = x; ctx->pos[1] = y; ctx->pos[2] = z; }
+        else if (nm == "u_mouse") { ctx->mouse[0] = x; ctx->mouse[1] = y; }
+        else if (nm == "u_time") ctx->time = x;
+        // u_sample_part, u_seed1, u_seed2: declared, unused by the pass (common.frag:8-11)
+        return RM_OK;
+    }
+    if (ctx->warned.insert(nm).second) std::fprintf(stderr, "rm: uniform \"%s\" not found in shader\n", name);
+    return RM_OK;
+}
+
+rm_status rm_set_uniform1f(rm_ctx *ctx, const char *name, float x) { return set_uniform(ctx, name, 1, x, 0, 0); }
+rm_status rm_set_uniform2f(rm_ctx *ctx, const char *name, float x, float y) {
+    return set_uniform(ctx, name, 2, x, y, 0);
+}
+rm_status rm_set_uniform3f(rm_ctx *ctx, const char *name, float x, float y, float z) {
+    return set_uniform(ctx, name, 3, x, y, z);
+}
+
+rm_status rm_set_params(rm_ctx *ctx, const rm_params *p) {
+    if (!ctx || !p) return RM_ERR_INVALID_ARGUMENT;
+    if (p->max_steps < 0 || p->max_steps > (1 << 20) || p->shadow_max_steps < 0 || p->kernel < 0 || p->kernel > 2)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_set_params: out of range");
+    ctx->params = *p;
+    return RM_OK;
+}
+
+rm_status rm_get_params(rm_ctx *ctx, rm_params *p) {
+    if (!ctx || !p) return RM_ERR_INVALID_ARGUMENT;
+    *p = ctx->params;
+    return RM_OK;
+}
+
+rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    ctx->stream = reinterpret_cast<hipStream_t>(stream);
+    return RM_OK;
+}
+
+rm_status rm_synchronize(rm_ctx *ctx) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    RM_HIP(hipStreamSynchronize(ctx->stream));
+    return RM_OK;
+}
+
+rm_status rm_render(rm_ctx *ctx, int W, int H, float *out, rm_stats *stats) {
+    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, out, stats);
+}
+
+rm_status rm_render_band(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out, rm_stats *stats) {
+    return render_any(ctx, W, H, band, nshards, shard, out, stats);
+}
+
+rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows) {
+    if (!nrows || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards) return RM_ERR_INVALID_ARGUMENT;
+    *nrows = rows_of_shard(H, band, nshards, shard);
+    return RM_OK;
+}
+
+static rm_status deinterleave_any(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
+                                  const void *gathered, void *out, bool rgba8) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!gathered || !out || W <= 0 || H <= 0 || band <= 0 || nshards <= 0)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave: bad arguments");
+    for (int s = 0; s < nshards; s++)
+        if (rows_of_shard(H, band, nshards, s) > rows_per_shard)
+            return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave: rows_per_shard too small");
+    if (!is_device_ptr(gathered) || !is_device_ptr(out))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rgba8 ? rm::launch_deinterleave_u32(reinterpret_cast<const uint32_t *>(gathered),
+                                                      reinterpret_cast<uint32_t *>(out), W, H, band, nshards,
+                                                      rows_per_shard, ctx->stream)
+                         : rm::launch_deinterleave(reinterpret_cast<const float4 *>(gathered),
+                                                   reinterpret_cast<float4 *>(out), W, H, band, nshards,
+                                                   rows_per_shard, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "deinterleave launch");
+    return RM_OK;
+}
+
+rm_status rm_deinterleave(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard, const float *gathered,
+                          float *out) {
+    return deinterleave_any(ctx, W, H, band, nshards, rows_per_shard, gathered, out, false);
+}
+
+rm_status rm_deinterleave_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
+                                const uint32_t *gathered, uint32_t *out) {
+    return deinterleave_any(ctx, W, H, band, nshards, rows_per_shard, gathered, out, true);
+}
+
+rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t *out) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!in || !out || npixels < 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_pack_rgba8: bad arguments");
+    if (!is_device_ptr(in) || !is_device_ptr(out))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_pack_rgba8: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_pack_rgba8(reinterpret_cast<const float4 *>(in), out, (size_t)npixels, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pack launch");
+    return RM_OK;
+}
+
+rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!out || W <= 0 || H <= 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rgba8: bad arguments");
+    RM_HIP(hipSetDevice(ctx->device));
+    size_t npx = (size_t)W * H;
+    size_t fbytes = npx * sizeof(float4), bbytes = npx * sizeof(uint32_t);
+    // staging holds the float frame, followed by the packed frame when `out` is host memory
+    bool dev_out = is_device_ptr(out);
+    rm_status s = ensure_staging(ctx, fbytes + (dev_out ? 0 : bbytes));
+    if (s != RM_OK) return s;
+    s = render_dev(ctx, W, H, H, 1, 0, ctx->staging, stats);
+    if (s != RM_OK) return s;
+    uint32_t *dst = dev_out ? out : reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(ctx->staging) + fbytes);
+    hipError_t e = rm::launch_pack_rgba8(ctx->staging, dst, npx, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pack launch");
+    if (!dev_out) {
+        RM_HIP(hipMemcpyAsync(out, dst, bbytes, hipMemcpyDeviceToHost, ctx->stream));
+        RM_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RM_OK;
+}
+
+const char *rm_last_error(rm_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+const char *rm_status_string(rm_status s) {
+    switch (s) {
+    case RM_OK: return "RM_OK";
+    case RM_ERR_INVALID_ARGUMENT: return "RM_ERR_INVALID_ARGUMENT";
+    case RM_ERR_FILE: return "RM_ERR_FILE";
+    case RM_ERR_SCENE: return "RM_ERR_SCENE";
+    case RM_ERR_NO_SCENE: return "RM_ERR_NO_SCENE";
+    case RM_ERR_DEVICE: return "RM_ERR_DEVICE";
+    case RM_ERR_OUT_OF_MEMORY: return "RM_ERR_OUT_OF_MEMORY";
+    }
+    return "RM_ERR_UNKNOWN";
+}
+
+}  // extern "C"

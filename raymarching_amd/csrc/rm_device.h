@@ -1,0 +1,265 @@
+// rm_device.h -- gfx950 device code for the SDF sphere-tracing pass.
+//
+// Scene distance functions, materials and shading terms of the reference's
+// fragment pass (cahekp/Raymarching common.frag + output_shader.frag +
+// template.frag), restructured for CDNA4:
+//   * per-frame constants (camera rotations, transformR's rotation, the 32
+//     Hash11 sample lengths of CalculateThickness) are computed once on the
+//     host and arrive in the kernel-argument segment (SGPRs), instead of being
+//     rebuilt per sceneSDF call (the reference builds three mat4 per call,
+//     common.frag:434-441);
+//   * marching loops evaluate the distance-only scene; the 16-float Material
+//     of scene O (common.frag:20-35) is evaluated once, at the point where a
+//     march stops, which is the point whose SdResult castRayD returns
+//     (common.frag:879-901);
+//   * phongContribForLight's getNormalFast(p) (common.frag:733) is the normal
+//     the caller already holds (same p, pure function) and is reused.
+// All arithmetic is IEEE f32 (GLSL float). GLSL min/max are fminf/fmaxf,
+// which agree with the GLSL definitions (y<x?y:x / x<y?y:x) whenever the NaN
+// can only be the second operand, as in every call site here.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rm {
+
+enum SceneId : int { SCENE_S0 = 0, SCENE_T = 1, SCENE_O = 2, SCENE_OG = 3 };
+
+constexpr float ZNEAR = 0.02f;   // common.frag:13
+constexpr float ZFAR = 50.0f;    // common.frag:14
+constexpr float PI_REF = 3.1416f;  // common.frag:1108
+
+// Per-frame constants. Passed by value as a kernel argument.
+struct FrameConst {
+    float res_x, res_y;            // u_resolution
+    float pos_x, pos_y, pos_z;     // u_pos
+    float cam1_c, cam1_s;          // rot(-u_mouse.y): cos, sin
+    float cam2_c, cam2_s;          // rot(u_mouse.x)
+    float ry_c, ry_s, rx_c, rx_s;  // transformR(.., vec3(180, 2*u_time, 0)): rotationY(-2t), rotationX(-180);
+                                   // rotationZ(-0) is the exact identity and is skipped
+    int W, H;                      // target size (gl_TexCoord = ((x+.5)/W, (y+.5)/H))
+    int band, nshards, shard;      // row y is rendered iff (y / band) % nshards == shard
+    int nrows;                     // rows of this shard (packed in increasing y)
+    int max_steps;                 // MAX_MARCHING_STEPS (common.frag:15), run-time
+    int shadow_max_steps;          // 0 = unbounded, as softshadow2 (common.frag:814)
+    float hash11[32];              // Hash11(i), i = 0..31 (output_shader.frag:54-59,102)
+};
+
+// ------------------------------------------------------------- vec3 helpers
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 v3s(float s) { return V3{s, s, s}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float length(V3 a) { return sqrtf(dot(a, a)); }
+__device__ __forceinline__ V3 normalize(V3 a) { return a * (1.0f / sqrtf(dot(a, a))); }
+__device__ __forceinline__ float clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+__device__ __forceinline__ float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+__device__ __forceinline__ V3 mix3(V3 x, V3 y, float a) {
+    return v3(gmix(x.x, y.x, a), gmix(x.y, y.y, a), gmix(x.z, y.z, a));
+}
+__device__ __forceinline__ float fract(float x) { return x - floorf(x); }
+__device__ __forceinline__ float smoothstep(float e0, float e1, float x) {
+    float t = clamp01((x - e0) / (e1 - e0));
+    return t * t * (3.0f - 2.0f * t);
+}
+// reflect(I,N) = I - 2*dot(N,I)*N
+__device__ __forceinline__ V3 reflect(V3 I, V3 N) { return I - N * (2.0f * dot(N, I)); }
+__device__ __forceinline__ V3 refract(V3 I, V3 N, float eta) {
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return v3s(0.0f);
+    return I * eta - N * (eta * d + sqrtf(k));
+}
+
+// ------------------------------------------------------------------ SDFs
+
+// GLSL mod(x, 2.0) = x - 2*floor(x/2)
+__device__ __forceinline__ float mod2(float x) { return x - 2.0f * floorf(x * 0.5f); }
+
+// mengersponge(p).x (common.frag:654-679) with sdBox(p, vec3(1)) (:595-600)
+__device__ __forceinline__ float menger(V3 p) {
+    float dx = fabsf(p.x) - 1.0f, dy = fabsf(p.y) - 1.0f, dz = fabsf(p.z) - 1.0f;
+    float mc = fmaxf(dx, fmaxf(dy, dz));
+    float ex = fmaxf(dx, 0.0f), ey = fmaxf(dy, 0.0f), ez = fmaxf(dz, 0.0f);
+    float d = fminf(mc, sqrtf(ex * ex + ey * ey + ez * ez));
+    float s = 1.0f;
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+        float ax = mod2(p.x * s) - 1.0f;
+        float ay = mod2(p.y * s) - 1.0f;
+        float az = mod2(p.z * s) - 1.0f;
+        s *= 3.0f;
+        float rx = fabsf(1.0f - 3.0f * fabsf(ax));
+        float ry = fabsf(1.0f - 3.0f * fabsf(ay));
+        float rz = fabsf(1.0f - 3.0f * fabsf(az));
+        float da = fmaxf(rx, ry), db = fmaxf(ry, rz), dc = fmaxf(rz, rx);
+        float c = (fminf(da, fminf(db, dc)) - 1.0f) / s;
+        d = fmaxf(d, c);  // if (c > d) d = c;
+    }
+    return d;
+}
+
+// transformR(p - vec3(0,3,0), vec3(180, 2t, 0)): row vector times rotationY
+// then rotationX (common.frag:434-441); rotation Z is the identity.
+__device__ __forceinline__ V3 sponge_space(const FrameConst& F, V3 p) {
+    float x = p.x, y = p.y - 3.0f, z = p.z;
+    float x1 = x * F.ry_c + z * F.ry_s;
+    float z1 = x * -F.ry_s + z * F.ry_c;
+    float y2 = y * F.rx_c + z1 * -F.rx_s;
+    float z2 = y * F.rx_s + z1 * F.rx_c;
+    return v3(x1, y2, z2);
+}
+
+// sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4
+__device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& m) {
+    float h = fmaxf(k - fabsf(a - b), 0.0f) / k;
+    m = h * h * h * 0.5f;
+    float s = m * k * (1.0f / 3.0f);
+    return (a < b ? a : b) - s;
+}
+
+// cube(vec4(c, r), p) (common.frag:589-593)
+__device__ __forceinline__ float cube(V3 p, V3 c, float r) {
+    float qx = fabsf(p.x - c.x) - r, qy = fabsf(p.y - c.y) - r, qz = fabsf(p.z - c.z) - r;
+    float ex = fmaxf(qx, 0.0f), ey = fmaxf(qy, 0.0f), ez = fmaxf(qz, 0.0f);
+    return sqrtf(ex * ex + ey * ey + ez * ez) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f);
+}
+
+// Scene distances ("one ray-step" = one call).
+template <int SC>
+__device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p);
+
+template <>
+__device__ __forceinline__ float scene_dist<SCENE_S0>(const FrameConst&, V3 p) {
+    return length(p - v3(0.0f, 1.0f, -3.0f)) - 1.0f;
+}
+template <>
+__device__ __forceinline__ float scene_dist<SCENE_T>(const FrameConst& F, V3 p) {
+    return menger(sponge_space(F, p));  // template.frag:41 (repaired)
+}
+// output_shader.frag:38-48
+__device__ __forceinline__ float scene_dist_O(const FrameConst& F, V3 p) {
+    float d0 = menger(sponge_space(F, p));
+    float d1 = length(p - v3(3.0f, 2.0f, 3.0f)) - 1.0f;
+    float d2 = cube(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+    float d3 = p.y;
+    float m;
+    float t1 = smin_cubic_d(d1, d2, 0.5f, m);
+    float t2 = smin_cubic_d(t1, d3, 0.5f, m);
+    return smin_cubic_d(d0, t2, 0.33f, m);
+}
+template <>
+__device__ __forceinline__ float scene_dist<SCENE_O>(const FrameConst& F, V3 p) { return scene_dist_O(F, p); }
+template <>
+__device__ __forceinline__ float scene_dist<SCENE_OG>(const FrameConst& F, V3 p) { return scene_dist_O(F, p); }
+
+// ------------------------------------------------------------- materials
+
+struct Mat {
+    V3 diffuse, specular;
+    float shininess, reflectivity, transparency;
+    V3 absorption;
+    float ior;
+    V3 emission;
+};
+
+__device__ __forceinline__ Mat mat_make(V3 d, V3 s, float sh, float refl, float tr, V3 ab, float ior, V3 em) {
+    Mat m;
+    m.diffuse = d; m.specular = s; m.shininess = sh; m.reflectivity = refl; m.transparency = tr;
+    m.absorption = ab; m.ior = ior; m.emission = em;
+    return m;
+}
+__device__ __forceinline__ Mat mat_red() {  // output_shader.frag:12
+    return mat_make(v3(0.2f, 0.02f, 0.02f), v3(0.04f, 0.02f, 0.02f), 32.0f, 0.0f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
+}
+__device__ __forceinline__ Mat mat_blue(bool glass) {  // output_shader.frag:14 (glass: test scene OG)
+    return mat_make(v3(0.02f, 0.02f, 0.2f), v3(0.02f, 0.02f, 0.04f), 32.0f, 0.0f, glass ? 0.9f : 0.0f,
+                    v3(2.0f, 2.0f, 0.75f) * 0.2f, 1.52f, v3(0.0f, 0.0f, 100.0f));
+}
+__device__ __forceinline__ Mat mat_mirror() {  // output_shader.frag:15
+    return mat_make(v3s(0.1f), v3s(0.09f), 64.0f, 0.25f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
+}
+// output_shader.frag:16-28
+__device__ __forceinline__ Mat floor_mat(V3 pos) {
+    float scale = fmaxf(10.0f, powf(length(pos), 1.3f));
+    float tx = smoothstep(-0.005f, 0.005f, sinf(pos.x * PI_REF) / scale);
+    float ty = smoothstep(-0.005f, 0.005f, sinf(pos.z * PI_REF) / scale);
+    float tile = fminf(fmaxf(tx, ty), fmaxf(1.0f - tx, 1.0f - ty));
+    V3 color = mix3(v3s(0.3f), v3s(0.025f), tile);
+    return mat_make(color, v3s(0.03f), 128.0f, 0.0f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
+}
+// blendMaterial with ALLOW_MATERIAL_BLENDING (common.frag:37-53)
+__device__ __forceinline__ Mat blend(const Mat& a, const Mat& b, float k) {
+    return mat_make(mix3(a.diffuse, b.diffuse, k), mix3(a.specular, b.specular, k), gmix(a.shininess, b.shininess, k),
+                    gmix(a.reflectivity, b.reflectivity, k), gmix(a.transparency, b.transparency, k),
+                    mix3(a.absorption, b.absorption, k), gmix(a.ior, b.ior, k), mix3(a.emission, b.emission, k));
+}
+__device__ __forceinline__ Mat smin_mat(float a, const Mat& ma, float b, const Mat& mb, float m) {
+    return blend(ma, mb, a < b ? m : 1.0f - m);
+}
+
+// The material half of sceneSDF at p (evaluated once where a march stops).
+template <int SC>
+__device__ __forceinline__ Mat scene_mat(const FrameConst& F, V3 p) {
+    if constexpr (SC == SCENE_O || SC == SCENE_OG) {
+        constexpr bool glass = SC == SCENE_OG;
+        float d0 = menger(sponge_space(F, p));
+        float d1 = length(p - v3(3.0f, 2.0f, 3.0f)) - 1.0f;
+        float d2 = cube(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+        float d3 = p.y;
+        float m1, m2, m3;
+        float t1 = smin_cubic_d(d1, d2, 0.5f, m1);
+        Mat b = mat_blue(glass);
+        Mat mt1 = smin_mat(d1, b, d2, b, m1);
+        float t2 = smin_cubic_d(t1, d3, 0.5f, m2);
+        Mat mt2 = smin_mat(t1, mt1, d3, floor_mat(p), m2);
+        (void)smin_cubic_d(d0, t2, 0.33f, m3);
+        return smin_mat(d0, mat_mirror(), t2, mt2, m3);
+    } else {
+        (void)F; (void)p;
+        return mat_red();
+    }
+}
+
+// ---------------------------------------------------------- post-colour
+
+// common.frag:1044-1051
+__device__ __forceinline__ float tonemap1(float c, float e2) {
+    float col = c * 2.0f / (1.0f + c);
+    col = powf(col, 0.4545f);
+    col = powf(col, e2);
+    return col * 0.5f + 0.5f * col * col * (3.0f - 2.0f * col);
+}
+// tonemap -> contrast (common.frag:1067) -> vignette(.., 0.1) (:1072)
+__device__ __forceinline__ V3 post_colour(V3 c, float tcx, float tcy) {
+    V3 t = v3(tonemap1(c.x, 0.85f), tonemap1(c.y, 0.97f), tonemap1(c.z, 1.0f));
+    t = v3(smoothstep(0.15f, 1.1f, t.x), smoothstep(0.15f, 1.1f, t.y), smoothstep(0.15f, 1.1f, t.z));
+    float v = 0.5f + 0.5f * powf(16.0f * tcx * tcy * (1.0f - tcx) * (1.0f - tcy), 0.1f);
+    return t * v;
+}
+
+// common.frag:1032-1042 with be = bi = vec3(2) and the fog colour of the scenes
+__device__ __forceinline__ V3 apply_scattering(V3 color, V3 ro, V3 p) {
+    float d = 1.0f - clamp01(length(p - ro) / ZFAR);
+    float e = expf(-d * 2.0f);
+    return color * (1.0f - e) + v3(0.34f, 0.435f, 0.57f) * e;
+}
+// output_shader.frag:178-182
+__device__ __forceinline__ V3 background(V3 ro, V3 rd) { return apply_scattering(v3s(0.0f), ro, ro + rd * ZFAR); }
+
+// ------------------------------------------------------------ hashing
+
+// output_shader.frag:61-66
+__device__ __forceinline__ V3 hash33(V3 p3) {
+    p3 = v3(fract(p3.x * 443.897f), fract(p3.y * 441.423f), fract(p3.z * 437.195f));
+    float dd = dot(p3, v3(p3.y + 19.19f, p3.x + 19.19f, p3.z + 19.19f));
+    p3 = p3 + v3s(dd);
+    return v3(fract((p3.x + p3.y) * p3.z), fract((p3.x + p3.x) * p3.y), fract((p3.y + p3.x) * p3.x));
+}
+
+}  // namespace rm

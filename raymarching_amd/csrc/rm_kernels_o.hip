@@ -1,0 +1,19 @@
+// rm_kernels_o.hip -- render kernels of scene O (output_shader.frag) and its
+// glass test variant OG.  Built with -ffp-contract=off: scene O's subsurface
+// term hashes the surface normal with fract(x * 443.897) (output_shader.frag:
+// 54-81), which turns one-ulp differences of the normal into different sample
+// directions; without fused multiply-adds the marching and normals round like
+// the GLSL (and the oracle) and the image matches to ~1e-5 mean instead of
+// ~4e-4 (DESIGN.md "Parity policy").
+#include "rm_kernels_impl.h"
+
+namespace rm {
+
+hipError_t launch_scene_o(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
+    return launch_scene<SCENE_O>(F, out, evals, kernel, s);
+}
+hipError_t launch_scene_og(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
+    return launch_scene<SCENE_OG>(F, out, evals, kernel, s);
+}
+
+}  // namespace rm

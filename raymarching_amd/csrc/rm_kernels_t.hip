@@ -1,0 +1,13 @@
+// rm_kernels_t.hip -- render kernels of scenes S0 and T (FMA contraction on).
+#include "rm_kernels_impl.h"
+
+namespace rm {
+
+hipError_t launch_scene_s0(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
+    return launch_scene<SCENE_S0>(F, out, evals, kernel, s);
+}
+hipError_t launch_scene_t(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
+    return launch_scene<SCENE_T>(F, out, evals, kernel, s);
+}
+
+}  // namespace rm

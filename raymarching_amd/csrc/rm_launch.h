@@ -1,0 +1,22 @@
+// rm_launch.h -- host-side launcher interface between the C-ABI (rm_capi.cpp)
+// and the kernels (rm_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rm_device.h"
+
+namespace rm {
+
+enum KernelKind : int { KERNEL_DIRECT = 0, KERNEL_WAVE = 1 };
+
+hipError_t launch_render(int scene, const FrameConst& F, float4* out, unsigned long long* evals, int kernel,
+                         hipStream_t s);
+hipError_t launch_deinterleave(const float4* gathered, float4* out, int W, int H, int band, int nshards,
+                               int rows_per_shard, hipStream_t s);
+hipError_t launch_deinterleave_u32(const uint32_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
+                                   int rows_per_shard, hipStream_t s);
+hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStream_t s);
+bool has_wave_kernel_host(int scene);
+
+}  // namespace rm

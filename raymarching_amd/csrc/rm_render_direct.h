@@ -1,0 +1,296 @@
+// rm_render_direct.h -- per-pixel render pipelines, one lane = one pixel.
+//
+// Straight control flow per lane (march, normal, probes, shadow march, ...);
+// the loops of different lanes diverge and a wave pays the slowest lane of
+// every phase.  Kept as the simple reference kernel of the HIP path and for
+// scene O; scene T also has the wave-compacted state-machine kernel
+// (rm_render_wave.h).
+#pragma once
+#include "rm_device.h"
+
+namespace rm {
+
+// common.frag:697-708 (tetrahedral gradient, h = 0.001)
+template <int SC>
+__device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, uint32_t& cnt) {
+    const float h = 0.001f;
+    float d0 = scene_dist<SC>(F, p + v3(h, -h, -h));
+    float d1 = scene_dist<SC>(F, p + v3(-h, -h, h));
+    float d2 = scene_dist<SC>(F, p + v3(-h, h, -h));
+    float d3 = scene_dist<SC>(F, p + v3(h, h, h));
+    cnt += 4;
+    V3 g = v3(d0, -d0, -d0) + v3(-d1, -d1, d1);
+    g = g + v3(-d2, d2, -d2);
+    g = g + v3(d3, d3, d3);
+    return normalize(g);
+}
+
+// common.frag:879-901. Returns dist (depth on hit, -1 on miss, last SDF value
+// on step exhaustion) and the point whose SdResult is returned.
+template <int SC, bool INSIDE>
+__device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V3& last_q, uint32_t& cnt) {
+    float depth = ZNEAR;
+    float res = 0.0f;
+    last_q = ro;
+    for (int i = 0; i < F.max_steps; i++) {
+        V3 q = ro + rd * depth;
+        res = scene_dist<SC>(F, q);
+        cnt++;
+        last_q = q;
+        if (INSIDE) {  // castRayDI, common.frag:903-925
+            if (-res < 0.001f * depth) return depth;
+            depth -= res;
+        } else {
+            if (res < 0.001f * depth) return depth;
+            depth += res;
+        }
+        if (depth >= ZFAR) return -1.0f;
+    }
+    return res;
+}
+
+// common.frag:931-954 (scene T marcher): returns the point
+template <int SC>
+__device__ __forceinline__ V3 cast_ray(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+    float depth = ZNEAR;
+    V3 p = ro + rd * depth;
+    for (int i = 0; i < F.max_steps; i++) {
+        float dist = scene_dist<SC>(F, p);
+        cnt++;
+        if (dist < 0.001f) return p;
+        depth += dist;
+        p = ro + rd * depth;
+        if (depth >= ZFAR) return ro + rd * ZFAR;
+    }
+    return p;
+}
+
+// common.frag:810-831, k = 4
+template <int SC>
+__device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
+                                              uint32_t& cnt) {
+    const float k = 4.0f;
+    float res = 1.0f, ph = 1e20f;
+    int it = 0;
+    for (float t = mint; t < maxt;) {
+        if (F.shadow_max_steps > 0 && it++ >= F.shadow_max_steps) break;
+        float h = scene_dist<SC>(F, ro + rd * t);
+        cnt++;
+        if (h < 0.001f) return 0.0f;
+        float y = h * h / (2.0f * ph);
+        float d = sqrtf(h * h - y * y);
+        res = fminf(res, k * d / fmaxf(0.0f, t - y));
+        ph = h;
+        t += h * 0.1f + 0.001f;
+    }
+    return res;
+}
+
+// common.frag:850-866
+template <int SC>
+__device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, uint32_t& cnt) {
+    float sum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        V3 p = pos + (n * (float)(i + 1)) * 0.2f;
+        sum += (1.0f / (float)(1 << i)) * scene_dist<SC>(F, p);
+    }
+    cnt += 4;
+    // maxSum = sum_i 2^-i (i+1) 0.2, accumulated in f32 as the reference does
+    float maxSum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) maxSum += (1.0f / (float)(1 << i)) * (float)(i + 1) * 0.2f;
+    return sum / maxSum;
+}
+
+// common.frag:730-754 (N = the caller's normal)
+__device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 p, V3 eye, V3 lightPos, V3 N) {
+    V3 L = normalize(lightPos - p);
+    V3 V = normalize(eye - p);
+    V3 R = normalize(reflect(-L, N));
+    float dotLN = dot(L, N);
+    float dotRV = dot(R, V);
+    if (dotLN < 0.0f) return v3s(0.0f);
+    if (dotRV < 0.0f) return k_d * dotLN;
+    return k_d * dotLN + k_s * powf(dotRV, alpha);
+}
+
+__device__ __forceinline__ V3 shadow_pow(float sha) { return v3(powf(sha, 1.0f), powf(sha, 1.2f), powf(sha, 1.5f)); }
+
+// output_shader.frag:85-116
+template <int SC>
+__device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm, uint32_t& cnt) {
+    float th = 0.0f;
+    V3 nn = -norm;
+    for (int i = 0; i < 32; i++) {
+        float fi = (float)i;
+        float sl = F.hash11[i];
+        V3 rnd = normalize(hash33(nn + v3s(fi)) - v3s(0.5f));
+        V3 dir = rnd - (nn * 2.0f) * fminf(0.0f, dot(rnd, nn));  // reflectVector (:70-73)
+        th += sl + scene_dist<SC>(F, pos + dir * sl);
+    }
+    cnt += 32;
+    return clamp01(th * 0.03125f);
+}
+
+// output_shader.frag:127-176
+template <int SC>
+__device__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, uint32_t& cnt) {
+    const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
+    V3 Ld = lightPos - p;
+    V3 lightDir = normalize(Ld);
+    float occ = ao_real<SC>(F, p, n, cnt);
+    float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, length(Ld), cnt);
+    float sky = clamp01(0.5f + 0.5f * n.y);
+    float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
+    V3 shading = phong(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, p, ro, lightPos, phongN) * shadow_pow(sha);
+    shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
+    shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
+    float th = thickness<SC>(F, p, n, cnt);
+    V3 sssl = lightDir + n * 0.6f;
+    float sssdot = powf(clamp01(dot(-rd, -sssl)), 1.1f) * 0.3f;
+    shading = shading + v3s((sssdot + 0.3f) * th);
+    V3 color = mat.diffuse * shading + mat.emission;
+    return apply_scattering(color, ro, p);
+}
+
+// output_shader.frag:218-230
+__device__ __forceinline__ float fresnel(float n2, V3 normal, V3 incident, float reflectivity) {
+    float r0 = (1.0f - n2) / (1.0f + n2);
+    r0 *= r0;
+    float x = 1.0f + dot(normal, incident);
+    float r = r0 + (1.0f - r0) * x * x * x * x * x;
+    return (1.0f - reflectivity) * r + reflectivity;
+}
+
+// output_shader.frag:246-262
+template <int SC>
+__device__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+    V3 q;
+    float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
+    if (dist > 0.0f) {
+        Mat m = scene_mat<SC>(F, q);
+        V3 p = ro + rd * dist;
+        V3 n = normal_fast<SC>(F, p, cnt);
+        return light_O<SC>(F, m, ro, rd, p, n, n, cnt);
+    }
+    return background(ro, rd);
+}
+
+// output_shader.frag:298-343 (MAX_REFRACTIONS 4); live only in test scene OG
+template <int SC>
+__device__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption, uint32_t& cnt) {
+    V3 color = v3s(0.0f);
+    float invert = -1.0f;
+    float absorb = 0.0f;
+    for (int i = 0; i < 4; i++) {
+        V3 q;
+        float dist = invert < 0.0f ? cast_ray_d<SC, true>(F, ro, rd, q, cnt) : cast_ray_d<SC, false>(F, ro, rd, q, cnt);
+        if (invert < 0.0f) absorb += dist;
+        if (dist < 0.0f) {
+            if (invert > 0.0f) color = color + background(ro, rd);
+            break;
+        }
+        Mat m = scene_mat<SC>(F, q);
+        V3 p = ro + rd * dist;
+        V3 g = normal_fast<SC>(F, p, cnt);
+        V3 n = g * invert;
+        V3 ref = reflect(rd, n);
+        color = color + light_O<SC>(F, m, ro, ref, p, n, g, cnt);
+        if (invert > 0.0f) break;
+        float ior = invert < 0.0f ? m.ior : 1.0f / m.ior;
+        V3 raf = refract(rd, n, ior);
+        bool tif = raf.x == 0.0f && raf.y == 0.0f && raf.z == 0.0f;
+        rd = tif ? ref : raf;
+        ro = p + rd * (0.01f / fabsf(dot(rd, n)));
+        invert = tif ? invert : -invert;
+    }
+    return color * v3(expf(-absorption.x * absorb), expf(-absorption.y * absorb), expf(-absorption.z * absorb));
+}
+
+// output_shader.frag:348-385
+template <int SC>
+__device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+    V3 q;
+    float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
+    if (!(dist > 0.0f)) return background(ro, rd);
+    Mat m = scene_mat<SC>(F, q);
+    V3 p = ro + rd * dist;
+    V3 n = normal_fast<SC>(F, p, cnt);
+    V3 color = light_O<SC>(F, m, ro, rd, p, n, n, cnt);
+    float rf = fresnel(m.ior, n, rd, m.transparency > 0.0f ? 0.0f : m.reflectivity);
+    if (m.reflectivity > 0.0f) {
+        V3 r = reflect(rd, n);
+        color = color + (render_reflection<SC>(F, p + r * 0.001f, r, cnt) * rf) * m.reflectivity;
+    }
+    if constexpr (SC == SCENE_OG) {
+        if (m.transparency > 0.0f) {
+            V3 r = refract(rd, n, 1.0f / m.ior);
+            color = color + (render_refraction<SC>(F, p + r * 0.001f, r, m.absorption, cnt) * (1.0f - rf)) *
+                                m.transparency;
+        }
+    }
+    return color;
+}
+
+// template.frag:45-76 (scene T)
+__device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+    constexpr int SC = SCENE_T;
+    V3 p = cast_ray<SC>(F, ro, rd, cnt);
+    V3 n = normal_fast<SC>(F, p, cnt);
+    // getColorReflect (common.frag:991-1002); its dead nr normal is skipped
+    V3 rdir = reflect(rd, n);
+    V3 pr = cast_ray<SC>(F, p + rdir * 0.01f, rdir, cnt);
+    float c = clamp01(length(pr - p) / 3.0f);
+    const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
+    V3 Ld = lightPos - p;
+    V3 lightDir = normalize(Ld);
+    float occ = ao_real<SC>(F, p, n, cnt);
+    float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, length(Ld), cnt);
+    float sky = clamp01(0.5f + 0.5f * n.y);
+    float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
+    float fre = powf(clamp01(1.0f + dot(n, rd)), 2.0f);
+    V3 shading = phong(v3(1.64f, 1.27f, 0.99f), v3(1.0f, 1.0f, 0.0f), 1280.0f, p, ro, lightPos, n) * shadow_pow(sha);
+    shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
+    shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
+    shading = shading + v3s(fre * occ);
+    return apply_scattering(v3s(c) * shading, ro, p);
+}
+
+// BASELINE config-1 scene S0: castRayD + normal + lambert
+__device__ __forceinline__ V3 render_S0(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+    constexpr int SC = SCENE_S0;
+    V3 q;
+    float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
+    if (dist > 0.0f) {
+        V3 p = ro + rd * dist;
+        V3 n = normal_fast<SC>(F, p, cnt);
+        V3 lightDir = normalize(v3(20.0f, 50.0f, 0.0f) - p);
+        return v3(0.2f, 0.02f, 0.02f) * (0.1f + clamp01(dot(n, lightDir)));
+    }
+    return background(ro, rd);
+}
+
+// Camera (output_shader.frag:388-404): gl_TexCoord at the pixel centre
+__device__ __forceinline__ void camera_ray(const FrameConst& F, int x, int y, float& tcx, float& tcy, V3& ro, V3& rd) {
+    tcx = ((float)x + 0.5f) / (float)F.W;
+    tcy = ((float)y + 0.5f) / (float)F.H;
+    float ux = (tcx - 0.5f) * F.res_x / F.res_y;
+    float uy = (tcy - 0.5f) * F.res_y / F.res_y;
+    ro = v3(F.pos_x, F.pos_y, F.pos_z);
+    rd = normalize(v3(ux, -uy, -1.0f));
+    // rd.yz *= rot(-u_mouse.y); rd.xz *= rot(u_mouse.x)  (row vector x mat2(c,-s,s,c))
+    float y1 = rd.y * F.cam1_c + rd.z * -F.cam1_s;
+    float z1 = rd.y * F.cam1_s + rd.z * F.cam1_c;
+    float x2 = rd.x * F.cam2_c + z1 * -F.cam2_s;
+    float z2 = rd.x * F.cam2_s + z1 * F.cam2_c;
+    rd = v3(x2, y1, z2);
+}
+
+// local packed row j of this shard -> frame row y
+__device__ __forceinline__ int shard_row(const FrameConst& F, int j) {
+    int b = j / F.band, r = j - b * F.band;
+    return (b * F.nshards + F.shard) * F.band + r;
+}
+
+}  // namespace rm

@@ -1,0 +1,122 @@
+"""Row-sharded frames across GPUs (one process per GPU, RCCL over xGMI).
+
+Pixels are independent, so a frame shards by rows.  Rows are dealt to ranks
+in bands of ``band`` rows, round robin: rank r owns frame row y iff
+``(y // band) % nshards == r`` (cheap sky rows and expensive sponge / floor
+rows spread evenly).  Each rank renders its rows packed in
+increasing y (``rm_render_band``), optionally packs them to RGBA8
+(``rm_pack_rgba8``), and one gather brings every band to the root, where
+``rm_deinterleave`` writes the frame.  The gather is the only collective on
+the path (``torch.distributed.gather``; the "nccl" backend is RCCL).
+
+``ShardPlan`` is pure layout logic and is shared with the CPU (gloo) tests.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    W: int
+    H: int
+    band: int
+    nshards: int
+
+    def rows(self, shard: int) -> list[int]:
+        """Frame rows of `shard`, in packed (increasing) order."""
+        return [y for y in range(self.H) if (y // self.band) % self.nshards == shard]
+
+    def count(self, shard: int) -> int:
+        nb = -(-self.H // self.band)
+        n = 0
+        for b in range(shard, nb, self.nshards):
+            n += self.H - b * self.band if b == nb - 1 else self.band
+        return n
+
+    @property
+    def rows_per_shard(self) -> int:
+        """Rows of the gather slot of every shard (the largest shard)."""
+        return max(self.count(s) for s in range(self.nshards))
+
+    def slot_of_row(self, y: int) -> tuple[int, int]:
+        """(shard, packed row) holding frame row y."""
+        gb, r = divmod(y, self.band)
+        shard, lb = gb % self.nshards, gb // self.nshards
+        return shard, lb * self.band + r
+
+    def gathered_index(self):
+        """Flat index into the [nshards * rows_per_shard] gathered rows for every frame row."""
+        rps = self.rows_per_shard
+        return [s * rps + j for s, j in (self.slot_of_row(y) for y in range(self.H))]
+
+
+def gather_to_root(local, plan: ShardPlan, rank: int, group=None, out=None):
+    """Gather each rank's packed rows (padded to rows_per_shard) into a
+    [nshards, rows_per_shard, ...] tensor on rank 0 (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+
+    rps = plan.rows_per_shard
+    if local.shape[0] != rps:
+        raise ValueError(f"local band buffer must have rows_per_shard={rps} rows, has {local.shape[0]}")
+    if rank == 0:
+        if out is None:
+            out = torch.empty((plan.nshards,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        dist.gather(local, gather_list=list(out.unbind(0)), dst=0, group=group)
+        return out
+    dist.gather(local, gather_list=None, dst=0, group=group)
+    return None
+
+
+class DistributedFrame:
+    """One rank's share of a row-sharded frame on its GPU.
+
+    ``render()`` runs this rank's rows, gathers to rank 0 and (on rank 0)
+    de-interleaves the frame; everything is asynchronous on the current
+    stream.  ``fmt`` is "rgba8" (the displayed RenderTexture format, 4 B/px on
+    the wire) or "float4" (full gl_FragColor, 16 B/px, used by parity tests).
+    """
+
+    def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None):
+        import torch
+
+        self.r, self.rank, self.world, self.fmt, self.group = renderer, rank, world, fmt, group
+        # one shard: the packed rows are the frame rows (no de-interleave needed)
+        self.plan = ShardPlan(W, H, band if world > 1 else H, world)
+        dev = torch.device(f"cuda:{renderer.device}")
+        rps = self.plan.rows_per_shard
+        self.local = torch.empty((rps, W, 4), dtype=torch.float32, device=dev)
+        self.local8 = torch.empty((rps, W), dtype=torch.int32, device=dev) if fmt == "rgba8" else None
+        wire = self.local8 if fmt == "rgba8" else self.local
+        self.gathered = (torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev)
+                         if rank == 0 and world > 1 else None)
+        if world == 1:
+            self.frame = wire
+        elif rank == 0:
+            shape = (H, W) if fmt == "rgba8" else (H, W, 4)
+            self.frame = torch.empty(shape, dtype=wire.dtype, device=dev)
+        else:
+            self.frame = None
+
+    def render_local(self, stats=False):
+        p = self.plan
+        return self.r.render_band(p.W, p.H, p.band, p.nshards, self.rank, out=self.local, stats=stats)
+
+    def finish(self):
+        """Everything of a frame after the render kernel: pack, gather, de-interleave."""
+        p = self.plan
+        wire = self.local
+        if self.fmt == "rgba8":
+            self.r.pack_rgba8(self.local, out=self.local8)
+            wire = self.local8
+        if self.world == 1:
+            return self.frame
+        g = gather_to_root(wire, p, self.rank, group=self.group, out=self.gathered)
+        if self.rank == 0:
+            self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, g, out=self.frame)
+        return self.frame
+
+    def render(self):
+        self.render_local()
+        return self.finish()

@@ -1,0 +1,329 @@
+"""HIP path (librm.so on the MI355X) against the oracle and the reference-GLSL
+goldens.  Every render goes through the C ABI."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import raymarching_amd as rm
+from raymarching_amd import POSES, S0_POSE
+from tests.parity import assert_parity, diff_stats
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+
+
+@pytest.fixture(scope="module")
+def R(torch_cuda):
+    r = rm.Renderer(0)
+    yield r
+    r.close()
+
+
+def setup(r, scene, pose, steps=128, kernel="auto", res=None, shadow=0):
+    r.load_scene(rm.SCENE_FILES[scene])
+    r.set_pose(pose["pos"], pose["mouse"], pose["time"])
+    r.set_params(max_steps=steps, shadow_max_steps=shadow, count_evals=1, kernel=kernel)
+    if res is not None:
+        r.set_uniform("u_resolution", *res)
+
+
+def hip(r, W, H):
+    img, st = r.render(W, H, stats=True)
+    return img.cpu().numpy(), st
+
+
+def ref(scene, W, H, pose, steps=128, **kw):
+    return oracle.render(scene, W, H, pos=pose["pos"], mouse=pose["mouse"], time=pose["time"], max_steps=steps,
+                         **kw)
+
+
+def check_evals(st, ev, tol=5e-3):
+    tot = int(ev.sum(dtype=np.uint64))
+    assert abs(st["evals"] - tot) <= tol * tot + 4, (st["evals"], tot)
+
+
+# ------------------------------------------------------------ goldens
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_hip_matches_reference_glsl_golden(R, path):
+    z = np.load(path, allow_pickle=False)
+    m = json.loads(str(z["meta"]))
+    pose = dict(pos=m["pos"], mouse=m["mouse"], time=m["time"])
+    setup(R, m["scene"], pose, m["max_steps"])
+    img, st = hip(R, m["W"], m["H"])
+    assert_parity(m["scene"], img, z["rgba"], label="vs golden")
+    check_evals(st, z["evals"])
+    o, _ = ref(m["scene"], m["W"], m["H"], pose, m["max_steps"])
+    assert_parity(m["scene"], img, o, label="vs oracle")
+
+
+# ------------------------------------------------------- configs / poses
+
+
+def test_c1_sphere_256(R):
+    setup(R, "S0", S0_POSE, 64)
+    img, st = hip(R, 256, 256)
+    o, ev = ref("S0", 256, 256, S0_POSE, 64)
+    s = assert_parity("S0", img, o)
+    assert s["max"] < 1e-3
+    assert st["evals"] == int(ev.sum())
+
+
+@pytest.mark.parametrize("pose", list(POSES))
+def test_scene_T_poses(R, pose):
+    setup(R, "T", POSES[pose], 128)
+    img, st = hip(R, 192, 108)
+    o, ev = ref("T", 192, 108, POSES[pose], 128)
+    assert_parity("T", img, o, label=pose)
+    check_evals(st, ev)
+
+
+@pytest.mark.parametrize("pose", list(POSES))
+def test_scene_O_poses(R, pose):
+    setup(R, "O", POSES[pose], 128)
+    img, st = hip(R, 128, 96)
+    o, ev = ref("O", 128, 96, POSES[pose], 128)
+    assert_parity("O", img, o, label=pose)
+    check_evals(st, ev)
+
+
+@pytest.mark.parametrize("pose", ["P1", "P2", "P5", "P7"])
+def test_glass_variant_refraction_path(R, pose):
+    """Test scene OG: blue objects with transparency 0.9 drive renderRefraction
+    (output_shader.frag:298-343) and castRayDI (common.frag:903-925)."""
+    setup(R, "OG", POSES[pose], 128)
+    img, st = hip(R, 128, 96)
+    o, ev = ref("OG", 128, 96, POSES[pose], 128)
+    assert_parity("OG", img, o, label=pose)
+    check_evals(st, ev)
+
+
+def test_glass_variant_differs_where_blue_is_visible(R):
+    imgs = {}
+    for sc in ("O", "OG"):
+        o, _ = ref(sc, 96, 64, POSES["P5"], 128)
+        imgs[sc] = o
+    assert np.abs(imgs["O"] - imgs["OG"]).max() > 0.05  # the pose shows the sphere/cube
+
+
+@pytest.mark.parametrize("steps", [0, 1, 2, 7, 512])
+def test_max_steps_edges(R, steps):
+    for sc in ("T", "O"):
+        setup(R, sc, POSES["P0"], steps)
+        img, st = hip(R, 64, 40)
+        o, ev = ref(sc, 64, 40, POSES["P0"], steps)
+        assert_parity(sc, img, o, label=f"steps={steps}")
+        check_evals(st, ev)
+
+
+def test_shadow_step_cap(R):
+    setup(R, "O", POSES["P6"], 128, shadow=16)
+    img, st = hip(R, 96, 64)
+    o, ev = ref("O", 96, 64, POSES["P6"], 128, shadow_max_steps=16)
+    assert_parity("O", img, o)
+    check_evals(st, ev)
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 37), (53, 1), (37, 23), (17, 129), (250, 3)])
+def test_ragged_sizes(R, W, H):
+    for sc in ("T", "O"):
+        setup(R, sc, POSES["P2"], 128)
+        img, st = hip(R, W, H)
+        o, ev = ref(sc, W, H, POSES["P2"], 128)
+        s = diff_stats(img, o)
+        assert s["f1e2"] >= 0.99 or W * H < 100 and s["max"] < 5e-2, s
+        check_evals(st, ev, tol=2e-2)
+
+
+def test_u_resolution_independent_of_target(R):
+    """uv uses u_resolution (output_shader.frag:390); gl_TexCoord uses the target."""
+    setup(R, "T", POSES["P0"], 128, res=(1600.0, 900.0))
+    img, _ = hip(R, 96, 96)
+    o, _ = ref("T", 96, 96, POSES["P0"], 128, res=(1600.0, 900.0))
+    assert_parity("T", img, o)
+
+
+# ------------------------------------------------------ sharding / frames
+
+
+@pytest.mark.parametrize("W,H,band,n", [(64, 48, 16, 2), (64, 50, 7, 3), (96, 64, 16, 8), (40, 33, 1, 5)])
+def test_bands_and_deinterleave_reassemble_the_frame(R, torch_cuda, W, H, band, n):
+    torch = torch_cuda
+    from raymarching_amd.frame import ShardPlan
+    setup(R, "O", POSES["P1"], 128)
+    R.set_params(count_evals=0)
+    full = R.render(W, H)
+    plan = ShardPlan(W, H, band, n)
+    rps = plan.rows_per_shard
+    g = torch.zeros((n, rps, W, 4), dtype=torch.float32, device="cuda")
+    for s in range(n):
+        cnt = rm.shard_rows(H, band, n, s)
+        assert cnt == plan.count(s) == len(plan.rows(s))
+        R.render_band(W, H, band, n, s, out=g[s, :cnt])
+        # a band holds exactly the frame rows of that shard, bit for bit
+        assert torch.equal(g[s, :cnt], full[plan.rows(s)])
+    frame = R.deinterleave(W, H, band, n, rps, g)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full)
+    # RGBA8 frames de-interleave the same way
+    g8 = torch.zeros((n, rps, W), dtype=torch.int32, device="cuda")
+    for s in range(n):
+        R.pack_rgba8(g[s], out=g8[s])
+    f8 = R.deinterleave(W, H, band, n, rps, g8)
+    assert torch.equal(f8, R.pack_rgba8(full))
+
+
+def test_pack_rgba8_rounding(R, torch_cuda):
+    torch = torch_cuda
+    x = torch.tensor([[0.0, 1.0, 0.5, 1.0], [-1.0, 2.0, 0.25, 0.998], [float("nan"), 0.00196, 0.00197, 1.0]],
+                     device="cuda")
+    p = R.pack_rgba8(x).cpu().numpy().view(np.uint32)
+    b = [[(int(v) >> (8 * c)) & 255 for c in range(4)] for v in p]
+    assert b[0] == [0, 255, 128, 255]
+    assert b[1] == [0, 255, 64, 254]
+    assert b[2] == [0, 0, 1, 255]
+
+
+def test_render_rgba8_matches_pack(R, torch_cuda):
+    setup(R, "T", POSES["P3"], 128)
+    full = R.render(80, 60)
+    a = R.render_rgba8(80, 60)
+    assert torch_cuda.equal(a, R.pack_rgba8(full))
+    host = np.zeros((60, 80), np.uint32)
+    st = rm.lib().rm_render_rgba8(R._ctx, 80, 60, R._ptr(host), None)
+    assert st == 0
+    np.testing.assert_array_equal(host.view(np.int32), a.cpu().numpy())
+
+
+def test_host_output_buffer(R, torch_cuda):
+    setup(R, "T", POSES["P0"], 128)
+    dev = R.render(48, 32).cpu().numpy()
+    host = np.zeros((32, 48, 4), np.float32)
+    st = rm.lib().rm_render(R._ctx, 48, 32, R._ptr(host), None)
+    assert st == 0
+    np.testing.assert_array_equal(host, dev)
+
+
+def test_deterministic(R, torch_cuda):
+    setup(R, "O", POSES["P4"], 128)
+    a = R.render(128, 72)
+    b = R.render(128, 72)
+    assert torch_cuda.equal(a, b)
+
+
+def test_wave_and_direct_kernels_agree(R, torch_cuda):
+    for sc in ("S0", "T", "O"):
+        setup(R, sc, POSES["P5"] if sc != "S0" else S0_POSE, 128, kernel="direct")
+        a, sa = R.render(96, 80, stats=True)
+        R.set_params(kernel="auto")
+        b, sb = R.render(96, 80, stats=True)
+        s = diff_stats(a.cpu().numpy(), b.cpu().numpy())
+        assert s["f1e2"] >= 0.999 and s["mean"] < 1e-4, (sc, s)
+        assert abs(sa["evals"] - sb["evals"]) <= 2e-3 * sa["evals"]
+
+
+# --------------------------------------------------- the reference surface
+
+
+def test_shader_loader_surface(torch_cuda, tmp_path, capsys):
+    sh = rm.Shader(0)
+    assert rm.ShaderLoader.loadFromFile("output_shader.frag", rm.Shader.Fragment, sh)
+    sh.setUniform("u_resolution", (64.0, 48.0))
+    sh.setUniform("u_pos", (2.0, 3.0, 3.0))
+    sh.setUniform("u_mouse", (0.0, 0.0))
+    sh.setUniform("u_time", 0.0)
+    sh.setUniform("u_sample_part", 1.0)     # declared, unused (common.frag:9)
+    sh.setUniform("u_seed1", (1.0, 2.0))
+    sh.setUniform("u_not_there", 1.0)       # warns once, ignored
+    tex = rm.RenderTexture()
+    tex.create(64, 48)
+    tex.draw(sh)
+    o, _ = ref("O", 64, 48, POSES["P0"], 128)
+    assert_parity("O", tex.getTexture().cpu().numpy(), o)
+    # missing file: false + the reference's message (source/shader_loader.cpp:28)
+    assert not rm.ShaderLoader.loadFromFile(str(tmp_path / "nope.frag"), rm.Shader.Fragment, sh)
+    err = capsys.readouterr().err
+    assert "can't load file" in err
+    # an existing file whose #include is missing fails like the reference
+    f = tmp_path / "template.frag"
+    f.write_text('#include "does_not_exist.frag"\nvoid main() {}\n')
+    assert not rm.ShaderLoader.loadFromFile(str(f), rm.Shader.Fragment, sh)
+    # an existing file of a registered name with resolvable includes loads
+    (tmp_path / "common.frag").write_text("// library\n")
+    f.write_text('#include <' + str(tmp_path / "common.frag") + '>\n// scene T\n')
+    assert rm.ShaderLoader.loadFromFile(str(f), rm.Shader.Fragment, sh)
+    # an unknown scene file exists but has no HIP plugin
+    u = tmp_path / "other.frag"
+    u.write_text("void main() {}\n")
+    assert not rm.ShaderLoader.loadFromFile(str(u), rm.Shader.Fragment, sh)
+    sh.close()
+
+
+def test_errors(torch_cuda):
+    r = rm.Renderer(0)
+    with pytest.raises(rm.RmError) as e:
+        r.render(8, 8)
+    assert e.value.status == 4  # RM_ERR_NO_SCENE
+    r.load_scene("template.frag")
+    with pytest.raises(rm.RmError) as e:
+        r.set_uniform("u_pos", 1.0, 2.0)
+    assert e.value.status == 1
+    with pytest.raises(rm.RmError):
+        r.set_params(max_steps=-1)
+    with pytest.raises(rm.RmError):
+        r.render_band(8, 8, 4, 2, 2)
+    with pytest.raises(ValueError):
+        r.render(8, 8, out=torch_cuda.empty(10, device="cuda"))
+    r.close()
+
+
+# ---------------------------------------------------------- full sizes
+
+
+def strided_parity(r, scene, W, H, pose, steps, stride, min_f2e3=None):
+    setup(r, scene, pose, steps)
+    r.set_params(count_evals=0)
+    img = r.render(W, H)
+    rows = np.arange(0, H, stride, dtype=np.int32)
+    sub = img[rows.tolist()].cpu().numpy()
+    o, _ = oracle.render_rows(scene, W, H, rows, pos=pose["pos"], mouse=pose["mouse"], time=pose["time"],
+                              max_steps=steps)
+    return assert_parity(scene, sub, o, label=f"{W}x{H} rows%{stride}"), img
+
+
+def test_c2_1080p_poses(R, torch_cuda):
+    for p in ("P0", "P3", "P8"):
+        strided_parity(R, "T", 1920, 1080, POSES[p], 128, 54)
+
+
+def test_c3_4096_properties(R, torch_cuda):
+    torch = torch_cuda
+    s, img = strided_parity(R, "T", 4096, 4096, POSES["P0"], 256, 128)
+    # determinism and exact reassembly from 8 row-interleaved shards (C4 layout)
+    from raymarching_amd.frame import ShardPlan
+    plan = ShardPlan(4096, 4096, 16, 8)
+    g = torch.empty((8, plan.rows_per_shard, 4096, 4), dtype=torch.float32, device="cuda")
+    for sh in range(8):
+        R.render_band(4096, 4096, 16, 8, sh, out=g[sh])
+    frame = R.deinterleave(4096, 4096, 16, 8, plan.rows_per_shard, g)
+    assert torch.equal(frame, img)
+    assert torch.isfinite(img).all()
+    assert torch.all(img[..., 3] == 1.0)
+    # ray-step count of the full frame vs the oracle's count on the sampled rows
+    R.set_params(count_evals=1)
+    _, st = R.render(4096, 4096, out=img, stats=True)
+    rows = np.arange(0, 4096, 128, dtype=np.int32)
+    _, ev = oracle.render_rows("T", 4096, 4096, rows, pos=POSES["P0"]["pos"], mouse=POSES["P0"]["mouse"],
+                               time=0.0, max_steps=256)
+    per_px_sample = float(ev.mean())
+    assert abs(st["evals"] / 4096 ** 2 - per_px_sample) / per_px_sample < 0.05
+
+
+def test_c5_8192_scene_O(R, torch_cuda):
+    strided_parity(R, "O", 8192, 8192, POSES["P0"], 512, 1024)

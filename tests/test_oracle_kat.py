@@ -1,0 +1,109 @@
+"""Closed-form known-answer tests of the oracle's SDF library (GLSL
+semantics of common.frag).  No reference fixtures exist for these; values are
+exact by construction."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+
+
+@pytest.fixture(scope="module")
+def L():
+    return oracle.lib()
+
+
+def test_glsl_mod_is_floor_based(L):
+    # GLSL mod(x, y) = x - y * floor(x / y): result has the sign of y
+    assert L.oracle_glsl_mod(-0.5, 2.0) == pytest.approx(1.5)
+    assert L.oracle_glsl_mod(3.5, 2.0) == pytest.approx(1.5)
+    assert L.oracle_glsl_mod(-4.0, 2.0) == 0.0
+    assert math.fmod(-0.5, 2.0) == -0.5  # C fmod differs
+
+
+def test_smoothstep(L):
+    assert L.oracle_glsl_smoothstep(0.0, 1.0, -1.0) == 0.0
+    assert L.oracle_glsl_smoothstep(0.0, 1.0, 2.0) == 1.0
+    assert L.oracle_glsl_smoothstep(0.0, 1.0, 0.5) == pytest.approx(0.5)
+    assert L.oracle_glsl_smoothstep(0.15, 1.1, 0.15) == 0.0
+
+
+def test_sphere_and_boxes(L):
+    assert L.oracle_sphere(0, 1, -1, 0, 1, -3, 1) == pytest.approx(1.0)
+    assert L.oracle_sphere(0, 1, -3, 0, 1, -3, 1) == pytest.approx(-1.0)
+    # cube: exact euclidean box distance; inside -> negative max component
+    assert L.oracle_cube(-5, 4, 8, -5, 4, 5, 1) == pytest.approx(2.0)
+    assert L.oracle_cube(-3, 6, 5, -5, 4, 5, 1) == pytest.approx(math.sqrt(2.0))
+    assert L.oracle_cube(-5, 4, 5, -5, 4, 5, 1) == pytest.approx(-1.0)
+    # sdBox (common.frag:595-600) is min(max-component, outside length)
+    assert L.oracle_sdbox(3, 0, 0, 1, 1, 1) == pytest.approx(2.0)
+    assert L.oracle_sdbox(3, 3, 0, 1, 1, 1) == pytest.approx(2.0)  # min(2, 2.83)
+    assert L.oracle_sdbox(0, 0, 0, 1, 1, 1) == pytest.approx(-1.0)
+
+
+def test_menger_sponge(L):
+    # far outside: the bounding box term dominates
+    assert L.oracle_menger(5, 0, 0) == pytest.approx(4.0)
+    # the centre lies in the first-level cross hole: distance (1-1/3*... ) > 0
+    assert L.oracle_menger(0, 0, 0) > 0.0
+    # a corner of the cube is solid (inside, d < 0)
+    assert L.oracle_menger(0.95, 0.95, 0.95) < 0.0
+
+
+def test_smin_cubic(L):
+    # |a-b| >= k: plain min
+    assert L.oracle_smin_cubic(1.0, 3.0, 0.5) == 1.0
+    assert L.oracle_smin_cubic(3.0, 1.0, 0.5) == 1.0
+    # a == b: min - k/6
+    assert L.oracle_smin_cubic(1.0, 1.0, 0.6) == pytest.approx(1.0 - 0.6 / 6.0, rel=1e-6)
+
+
+def test_sphere_scene_normal_points_outward():
+    pts = np.array([[0, 2, -3], [1, 1, -3], [0, 1, -2]], np.float32)
+    n = oracle.normal("S0", pts)
+    exp = np.array([[0, 1, 0], [1, 0, 0], [0, 0, 1]], np.float32)
+    np.testing.assert_allclose(n, exp, atol=2e-3)
+
+
+def test_scene_distances_consistent():
+    pts = np.array([[0, 3, 0], [3, 2, 3], [-5, 4, 5], [10, 0.5, 10]], np.float32)
+    dT = oracle.scene_dist("T", pts, time=0.0)
+    dO = oracle.scene_dist("O", pts, time=0.0)
+    assert dT[0] == pytest.approx(float(oracle.lib().oracle_menger(0, 0, 0)), abs=1e-6)
+    assert dO[1] < 0 and dO[2] < 0  # inside sphere / cube
+    assert dO[3] == pytest.approx(0.5, abs=1e-6)  # floor plane
+
+
+def test_hash11_range(L):
+    v = [L.oracle_hash11(float(i)) for i in range(32)]
+    assert all(0.0 <= x < 1.0 for x in v)
+    assert len(set(v)) > 28
+
+
+def test_step_counts_and_exhaustion():
+    # scene T, 1 step: each of the 2 marches makes exactly 1 call, plus the
+    # normal (4), AO (4) and >= 1 shadow step
+    img1, ev1 = oracle.render("T", 16, 16, max_steps=1)
+    assert ev1.min() >= 2 + 4 + 4 + 1
+    assert np.isfinite(img1).all()
+    # step-exhausted castRayD returns the last SDF value as the hit distance
+    # (common.frag:900): the image changes with the cap
+    img2, _ = oracle.render("O", 16, 16, max_steps=2)
+    img3, _ = oracle.render("O", 16, 16, max_steps=128)
+    assert np.abs(img2 - img3).max() > 1e-2
+
+
+def test_row_subsets_equal_full_frame():
+    full, ev = oracle.render("O", 24, 20)
+    part, evp = oracle.render("O", 24, 20, row0=7, nrows=5)
+    np.testing.assert_array_equal(part, full[7:12])
+    rows, evr = oracle.render_rows("O", 24, 20, [3, 19, 0])
+    np.testing.assert_array_equal(rows, full[[3, 19, 0]])
+    np.testing.assert_array_equal(evr, ev[[3, 19, 0]])
+
+
+def test_shadow_cap_only_shortens():
+    _, ev0 = oracle.render("T", 32, 32, shadow_max_steps=0)
+    _, ev1 = oracle.render("T", 32, 32, shadow_max_steps=8)
+    assert ev1.sum() <= ev0.sum()
