@@ -72,7 +72,31 @@ typedef struct {
      * rotationX/Y/Z compute them (radians(), cos(), sin()). */
     float ry_c, ry_s, rx_c, rx_s, rz_c, rz_s;
     uint64_t *evals; /* per-thread counter of sceneSDF calls */
+    struct SegRec *rec; /* optional: per-pixel phase/segment recorder (analysis) */
 } Ctx;
+
+/* Analysis aid (not part of the restatement): records, per pixel, the
+ * sequence of sceneSDF-call segments as (phase, count) pairs, so the SIMD
+ * efficiency of lane-per-pixel vs. wave-compacted schedules can be simulated
+ * (tools/wave_sim.py).  Phases: 0 march, 1 normal, 2 AO, 3 shadow, 4 SSS. */
+enum { PH_MARCH = 0, PH_NORMAL = 1, PH_AO = 2, PH_SHADOW = 3, PH_SSS = 4 };
+#define MAX_SEG 24
+typedef struct SegRec {
+    int phase, fresh, nseg;
+    uint16_t *out; /* MAX_SEG x (phase, count) */
+} SegRec;
+static inline void seg_begin(const Ctx *C, int phase) {
+    if (C->rec) { C->rec->phase = phase; C->rec->fresh = 1; }
+}
+static inline void seg_eval(SegRec *r) {
+    if (!r->fresh && r->nseg > 0) { r->out[2 * (r->nseg - 1) + 1]++; return; }
+    if (r->nseg < MAX_SEG) {
+        r->out[2 * r->nseg] = (uint16_t)r->phase;
+        r->out[2 * r->nseg + 1] = 1;
+        r->nseg++;
+    }
+    r->fresh = 0;
+}
 
 /* --------------------------------------------------------- GLSL built-ins */
 
@@ -279,6 +303,7 @@ static SdResult sceneSDF_O(const Ctx *C, vec3 p) {
 
 static SdResult sceneSDF(const Ctx *C, vec3 p) {
     (*C->evals)++;
+    if (C->rec) seg_eval(C->rec);
     switch (C->scene) {
     case SCENE_S0: return sceneSDF_S0(C, p);
     case SCENE_T: return sceneSDF_T(C, p);
@@ -290,6 +315,7 @@ static SdResult sceneSDF(const Ctx *C, vec3 p) {
 
 /* common.frag:697-708 */
 static vec3 getNormalFast(const Ctx *C, vec3 p) {
+    seg_begin(C, PH_NORMAL);
     const float h = 0.001f;
     const vec3 k0 = v3(1.0f, -1.0f, -1.0f);
     const vec3 k1 = v3(-1.0f, -1.0f, 1.0f);
@@ -323,6 +349,7 @@ static vec3 phongContribForLight(vec3 k_d, vec3 k_s, float alpha, vec3 p, vec3 e
 
 /* common.frag:810-831.  max_steps == 0: unbounded, as the reference. */
 static float softshadow2(const Ctx *C, vec3 ro, vec3 rd, float mint, float maxt, float k) {
+    seg_begin(C, PH_SHADOW);
     float res = 1.0f;
     float ph = 1e20f;
     int it = 0;
@@ -341,6 +368,7 @@ static float softshadow2(const Ctx *C, vec3 ro, vec3 rd, float mint, float maxt,
 
 /* common.frag:850-866 (_AOSteps = 4, _AOStepSize = 0.2) */
 static float ambientOcclusionReal(const Ctx *C, vec3 pos, vec3 normal) {
+    seg_begin(C, PH_AO);
     float sum = 0.0f;
     float maxSum = 0.0f;
     for (int i = 0; i < 4; i++) {
@@ -353,6 +381,7 @@ static float ambientOcclusionReal(const Ctx *C, vec3 pos, vec3 normal) {
 
 /* common.frag:879-901 */
 static SdResult castRayD(const Ctx *C, vec3 ro, vec3 rd) {
+    seg_begin(C, PH_MARCH);
     SdResult res;
     memset(&res, 0, sizeof(res));
     float depth = ZNEAR;
@@ -373,6 +402,7 @@ static SdResult castRayD(const Ctx *C, vec3 ro, vec3 rd) {
 
 /* common.frag:903-925 */
 static SdResult castRayDI(const Ctx *C, vec3 ro, vec3 rd) {
+    seg_begin(C, PH_MARCH);
     SdResult res;
     memset(&res, 0, sizeof(res));
     float depth = ZNEAR;
@@ -393,6 +423,7 @@ static SdResult castRayDI(const Ctx *C, vec3 ro, vec3 rd) {
 
 /* common.frag:931-954 */
 static vec3 castRay(const Ctx *C, vec3 ro, vec3 rd) {
+    seg_begin(C, PH_MARCH);
     float depth = ZNEAR;
     vec3 p = add(ro, muls(rd, depth));
     for (int i = 0; i < C->u.max_steps; i++) {
@@ -478,6 +509,7 @@ static vec3 GenerateSampleVector(vec3 norm, float i) {
 
 /* output_shader.frag:85-116 */
 static float CalculateThickness(const Ctx *C, vec3 pos, vec3 norm) {
+    seg_begin(C, PH_SSS);
     const float SSSSampleDepth = 1.0f;
     const float SSSThicknessSamples = 32.0f;
     const float SSSThicknessSamplesI = 0.03125f;
@@ -728,6 +760,32 @@ int oracle_render_rows(int scene, const oracle_uniforms *u, int W, int H, const 
             uint64_t before = cnt;
             shade_pixel(&C, W, H, x, rows[r], out + ((size_t)r * W + x) * 4);
             if (evals) evals[(size_t)r * W + x] = (uint32_t)(cnt - before);
+        }
+    }
+    return 0;
+}
+
+/* Per-pixel sceneSDF segments (analysis aid): seg = nrows*W*MAX_SEG*2 u16,
+ * nseg = nrows*W u8. */
+int oracle_render_segments(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, uint16_t *seg,
+                           uint8_t *nseg) {
+    if (!u || !seg || !nseg || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H) return 1;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; r++) {
+        Ctx C;
+        uint64_t cnt = 0;
+        SegRec rec;
+        float px[4];
+        init_ctx(&C, scene, u);
+        C.evals = &cnt;
+        C.rec = &rec;
+        for (int x = 0; x < W; x++) {
+            size_t i = (size_t)r * W + x;
+            memset(&rec, 0, sizeof(rec));
+            rec.out = seg + i * MAX_SEG * 2;
+            memset(rec.out, 0, MAX_SEG * 2 * sizeof(uint16_t));
+            shade_pixel(&C, W, H, x, row0 + r, px);
+            nseg[i] = (uint8_t)rec.nseg;
         }
     }
     return 0;

@@ -14,9 +14,7 @@
 //     (common.frag:879-901);
 //   * phongContribForLight's getNormalFast(p) (common.frag:733) is the normal
 //     the caller already holds (same p, pure function) and is reused.
-// All arithmetic is IEEE f32 (GLSL float). GLSL min/max are fminf/fmaxf,
-// which agree with the GLSL definitions (y<x?y:x / x<y?y:x) whenever the NaN
-// can only be the second operand, as in every call site here.
+// All arithmetic is IEEE f32 (GLSL float).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -57,7 +55,14 @@ __device__ __forceinline__ V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ float length(V3 a) { return sqrtf(dot(a, a)); }
 __device__ __forceinline__ V3 normalize(V3 a) { return a * (1.0f / sqrtf(dot(a, a))); }
-__device__ __forceinline__ float clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+// GLSL min/max/clamp by their spec definitions (min(x,y) = y < x ? y : x,
+// max(x,y) = x < y ? y : x), which differ from fminf/fmaxf only when x is NaN.
+// Shading code uses these (a NaN colour, e.g. pow() of a negative colour in
+// the glass test scene, must propagate as in the GLSL); the distance functions
+// use fminf/fmaxf, whose operands are never NaN for finite sample points.
+__device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
+__device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
+__device__ __forceinline__ float clamp01(float x) { return gmin(gmax(x, 0.0f), 1.0f); }
 __device__ __forceinline__ float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
 __device__ __forceinline__ V3 mix3(V3 x, V3 y, float a) {
     return v3(gmix(x.x, y.x, a), gmix(x.y, y.y, a), gmix(x.z, y.z, a));
@@ -78,27 +83,49 @@ __device__ __forceinline__ V3 refract(V3 I, V3 N, float eta) {
 
 // ------------------------------------------------------------------ SDFs
 
-// GLSL mod(x, 2.0) = x - 2*floor(x/2)
-__device__ __forceinline__ float mod2(float x) { return x - 2.0f * floorf(x * 0.5f); }
+// x / b for a constant b, correctly rounded in all but rare cases: one
+// Markstein refinement of x * RN(1/b) (3 VALU ops; the reference's divisions
+// are GLSL "/" with <= 2.5 ulp).  Used on the parity-critical scene-O path.
+__device__ __forceinline__ float div_const(float x, float b, float rb) {
+    float q = x * rb;
+    float r = fmaf(-b, q, x);
+    return fmaf(r, rb, q);
+}
 
-// mengersponge(p).x (common.frag:654-679) with sdBox(p, vec3(1)) (:595-600)
+// mengersponge(p).x (common.frag:654-679) with sdBox(p, vec3(1)) (:595-600).
+// Per fold, with xh = x*s/2 (exact: x*s*0.5 == x*(s/2)):
+//   mod(x*s, 2) - 1 == 2*(xh - floor(xh)) - 1   (bit-identical, one rounding)
+//   min(max(rx,ry), max(ry,rz), max(rz,rx)) == med3(rx, ry, rz)
+// EXACT keeps the reference's roundings (separate 1 - 3|a|, division by s);
+// the fast form fuses them (fma) and divides by s through a reciprocal.
+template <bool EXACT>
 __device__ __forceinline__ float menger(V3 p) {
     float dx = fabsf(p.x) - 1.0f, dy = fabsf(p.y) - 1.0f, dz = fabsf(p.z) - 1.0f;
     float mc = fmaxf(dx, fmaxf(dy, dz));
     float ex = fmaxf(dx, 0.0f), ey = fmaxf(dy, 0.0f), ez = fmaxf(dz, 0.0f);
-    float d = fminf(mc, sqrtf(ex * ex + ey * ey + ez * ez));
-    float s = 1.0f;
+    float l2 = ex * ex + ey * ey + ez * ez;
+    float d = fminf(mc, EXACT ? sqrtf(l2) : __builtin_amdgcn_sqrtf(l2));
+    constexpr float SH[3] = {0.5f, 1.5f, 4.5f};                      // s/2 before s *= 3
+    constexpr float S3[3] = {3.0f, 9.0f, 27.0f};                     // s after s *= 3
+    constexpr float INV[3] = {1.0f / 3.0f, 1.0f / 9.0f, 1.0f / 27.0f};
 #pragma unroll
     for (int m = 0; m < 3; m++) {
-        float ax = mod2(p.x * s) - 1.0f;
-        float ay = mod2(p.y * s) - 1.0f;
-        float az = mod2(p.z * s) - 1.0f;
-        s *= 3.0f;
-        float rx = fabsf(1.0f - 3.0f * fabsf(ax));
-        float ry = fabsf(1.0f - 3.0f * fabsf(ay));
-        float rz = fabsf(1.0f - 3.0f * fabsf(az));
-        float da = fmaxf(rx, ry), db = fmaxf(ry, rz), dc = fmaxf(rz, rx);
-        float c = (fminf(da, fminf(db, dc)) - 1.0f) / s;
+        float hx = p.x * SH[m], hy = p.y * SH[m], hz = p.z * SH[m];
+        float ax = fmaf(2.0f, hx - floorf(hx), -1.0f);
+        float ay = fmaf(2.0f, hy - floorf(hy), -1.0f);
+        float az = fmaf(2.0f, hz - floorf(hz), -1.0f);
+        float rx, ry, rz;
+        if constexpr (EXACT) {
+            rx = fabsf(1.0f - 3.0f * fabsf(ax));
+            ry = fabsf(1.0f - 3.0f * fabsf(ay));
+            rz = fabsf(1.0f - 3.0f * fabsf(az));
+        } else {
+            rx = fabsf(fmaf(-3.0f, fabsf(ax), 1.0f));
+            ry = fabsf(fmaf(-3.0f, fabsf(ay), 1.0f));
+            rz = fabsf(fmaf(-3.0f, fabsf(az), 1.0f));
+        }
+        float med = __builtin_amdgcn_fmed3f(rx, ry, rz);
+        float c = EXACT ? div_const(med - 1.0f, S3[m], INV[m]) : fmaf(med, INV[m], -INV[m]);
         d = fmaxf(d, c);  // if (c > d) d = c;
     }
     return d;
@@ -106,18 +133,27 @@ __device__ __forceinline__ float menger(V3 p) {
 
 // transformR(p - vec3(0,3,0), vec3(180, 2t, 0)): row vector times rotationY
 // then rotationX (common.frag:434-441); rotation Z is the identity.
+template <bool EXACT>
 __device__ __forceinline__ V3 sponge_space(const FrameConst& F, V3 p) {
     float x = p.x, y = p.y - 3.0f, z = p.z;
-    float x1 = x * F.ry_c + z * F.ry_s;
-    float z1 = x * -F.ry_s + z * F.ry_c;
-    float y2 = y * F.rx_c + z1 * -F.rx_s;
-    float z2 = y * F.rx_s + z1 * F.rx_c;
-    return v3(x1, y2, z2);
+    if constexpr (EXACT) {
+        float x1 = x * F.ry_c + z * F.ry_s;
+        float z1 = x * -F.ry_s + z * F.ry_c;
+        float y2 = y * F.rx_c + z1 * -F.rx_s;
+        float z2 = y * F.rx_s + z1 * F.rx_c;
+        return v3(x1, y2, z2);
+    } else {
+        float x1 = fmaf(x, F.ry_c, z * F.ry_s);
+        float z1 = fmaf(z, F.ry_c, -(x * F.ry_s));
+        float y2 = fmaf(y, F.rx_c, -(z1 * F.rx_s));
+        float z2 = fmaf(z1, F.rx_c, y * F.rx_s);
+        return v3(x1, y2, z2);
+    }
 }
 
 // sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4
 __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& m) {
-    float h = fmaxf(k - fabsf(a - b), 0.0f) / k;
+    float h = div_const(fmaxf(k - fabsf(a - b), 0.0f), k, 1.0f / k);
     m = h * h * h * 0.5f;
     float s = m * k * (1.0f / 3.0f);
     return (a < b ? a : b) - s;
@@ -140,11 +176,11 @@ __device__ __forceinline__ float scene_dist<SCENE_S0>(const FrameConst&, V3 p) {
 }
 template <>
 __device__ __forceinline__ float scene_dist<SCENE_T>(const FrameConst& F, V3 p) {
-    return menger(sponge_space(F, p));  // template.frag:41 (repaired)
+    return menger<false>(sponge_space<false>(F, p));  // template.frag:41 (repaired)
 }
 // output_shader.frag:38-48
 __device__ __forceinline__ float scene_dist_O(const FrameConst& F, V3 p) {
-    float d0 = menger(sponge_space(F, p));
+    float d0 = menger<true>(sponge_space<true>(F, p));
     float d1 = length(p - v3(3.0f, 2.0f, 3.0f)) - 1.0f;
     float d2 = cube(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
     float d3 = p.y;
@@ -208,7 +244,7 @@ template <int SC>
 __device__ __forceinline__ Mat scene_mat(const FrameConst& F, V3 p) {
     if constexpr (SC == SCENE_O || SC == SCENE_OG) {
         constexpr bool glass = SC == SCENE_OG;
-        float d0 = menger(sponge_space(F, p));
+        float d0 = menger<true>(sponge_space<true>(F, p));
         float d1 = length(p - v3(3.0f, 2.0f, 3.0f)) - 1.0f;
         float d2 = cube(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
         float d3 = p.y;

@@ -12,6 +12,6 @@ if [ $rc -ge 2 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 3; }
 cat gpurun_out/bench_$TAG.json
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python bench.py --cpu-seconds 0 --steps 10 ${BENCH_ARGS:-} > gpurun_out/bench_prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/bench_prof_$TAG.log; exit 4; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --cpu-seconds 0 --steps 10 ${BENCH_ARGS:-} > gpurun_out/bench_prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/bench_prof_$TAG.log; exit 4; }
 find gpurun_out/prof_$TAG -name "*stats*" | head
 exit $rc
