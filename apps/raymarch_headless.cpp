@@ -1,0 +1,128 @@
+// raymarch_headless.cpp -- the reference's frame loop (main.cpp:12-226)
+// without a window: the ray-march pass runs through rm::Shader /
+// rm::RenderTexture (include/rm_pass.hpp -> librm.so) exactly where main.cpp
+// calls ShaderLoader / sf::Shader::setUniform / RenderTexture::draw.
+//
+// Input comes from a script instead of SFML events: one character per frame,
+// W/A/S/D/U(p)/N(down) move as the reference's WASD/Space/LShift
+// (main.cpp:111-126,155-171), '.' = no key; --mouse dx,dy adds a per-frame
+// mouse delta (main.cpp:86-97).  The FXAA/bloom passes and the ImGui overlay
+// stay out of scope (they remain on the reference's GL path).
+//
+// Usage: raymarch_headless [--scene output_shader.frag] [--w 1600] [--h 900]
+//          [--frames 60] [--script WWWWDD..] [--mouse 3,0] [--time-freeze]
+//          [--steps 128] [--ppm out.ppm]
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../include/rm_pass.hpp"
+
+int main(int argc, char** argv) {
+    std::string scene = "output_shader.frag", script, ppm;
+    int w = 1600, h = 900, frames = 60, steps = 128;
+    int mdx = 0, mdy = 0;
+    bool time_freeze = false;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        auto next = [&]() { return i + 1 < argc ? std::string(argv[++i]) : std::string(); };
+        if (a == "--scene") scene = next();
+        else if (a == "--w") w = std::atoi(next().c_str());
+        else if (a == "--h") h = std::atoi(next().c_str());
+        else if (a == "--frames") frames = std::atoi(next().c_str());
+        else if (a == "--script") script = next();
+        else if (a == "--steps") steps = std::atoi(next().c_str());
+        else if (a == "--ppm") ppm = next();
+        else if (a == "--time-freeze") time_freeze = true;
+        else if (a == "--mouse") std::sscanf(next().c_str(), "%d,%d", &mdx, &mdy);
+        else {
+            std::fprintf(stderr, "unknown argument %s\n", a.c_str());
+            return 2;
+        }
+    }
+    // main.cpp:14-27
+    float wf = (float)w, hf = (float)h;
+    int mouseX = w / 2, mouseY = h / 2;
+    const float mouseSensitivity = 3.0f, speed = 0.1f;
+    rm::Vec3 pos{2.0f, 3.0f, 3.0f};
+    int framesStill = 1;
+
+    rm::RenderTexture outputTexture;
+    if (!outputTexture.create(w, h)) {
+        std::fprintf(stderr, "cannot allocate %dx%d target\n", w, h);
+        return 1;
+    }
+    rm::Shader shader;
+    if (!shader.valid()) {
+        std::fprintf(stderr, "no HIP device\n");
+        return 1;
+    }
+    if (!rm::ShaderLoader::loadFromFile(scene.c_str(), rm::Shader::Fragment, shader)) return 1;
+    shader.setUniform("u_resolution", rm::Vec2{wf, hf});
+    shader.setMarchSteps(steps);
+
+    std::mt19937 e2(20261015);
+    std::uniform_real_distribution<float> dist(0.0f, 1.0f);
+    auto t0 = std::chrono::steady_clock::now();
+    double kernel_ms = 0.0;
+    for (int f = 0; f < frames; f++) {
+        bool wasd[6] = {false, false, false, false, false, false};
+        char k = f < (int)script.size() ? script[f] : '.';
+        const char keys[] = "WASDUN";
+        for (int j = 0; j < 6; j++) wasd[j] = (k == keys[j]);
+        mouseX += mdx;
+        mouseY += mdy;
+        if (mdx || mdy) framesStill = 1;
+        // main.cpp:153-171: camera angles and a step along the view-rotated axes
+        float mx = ((float)mouseX / w - 0.5f) * mouseSensitivity;
+        float my = ((float)mouseY / h - 0.5f) * mouseSensitivity;
+        float dx = (float)(wasd[3] - wasd[1]), dy = (float)(wasd[4] - wasd[5]), dz = (float)(wasd[2] - wasd[0]);
+        float ty = dy * std::cos(-my) - dz * std::sin(-my);
+        float tz = dy * std::sin(-my) + dz * std::cos(-my);
+        float tx = dx;
+        float nx = tx * std::cos(mx) - tz * std::sin(mx);
+        float nz = tx * std::sin(mx) + tz * std::cos(mx);
+        pos = rm::Vec3{pos.x + nx * speed, pos.y + ty * speed, pos.z + nz * speed};
+        for (bool b : wasd)
+            if (b) framesStill = 1;
+        shader.setUniform("u_pos", pos);
+        shader.setUniform("u_mouse", rm::Vec2{mx, my});
+        if (!time_freeze) {
+            float t = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
+            shader.setUniform("u_time", t);
+        }
+        shader.setUniform("u_sample_part", 1.0f / framesStill);
+        shader.setUniform("u_seed1", rm::Vec2{dist(e2) * 999.0f, dist(e2) * 999.0f});
+        shader.setUniform("u_seed2", rm::Vec2{dist(e2) * 999.0f, dist(e2) * 999.0f});
+        rm_stats st;
+        if (!outputTexture.draw(shader, &st)) {
+            std::fprintf(stderr, "draw failed: %s\n", shader.lastError().c_str());
+            return 1;
+        }
+        kernel_ms += st.kernel_ms;
+        framesStill++;
+    }
+    double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("{\"frames\": %d, \"w\": %d, \"h\": %d, \"scene\": \"%s\", \"kernel_ms_per_frame\": %.4f, "
+                "\"fps_wall\": %.2f, \"pos\": [%.4f, %.4f, %.4f]}\n",
+                frames, w, h, scene.c_str(), frames ? kernel_ms / frames : 0.0, frames / wall, pos.x, pos.y, pos.z);
+    if (!ppm.empty()) {
+        std::vector<uint32_t> px;
+        if (!outputTexture.copyToHostRGBA8(shader, px)) return 1;
+        FILE* fp = std::fopen(ppm.c_str(), "wb");
+        if (!fp) return 1;
+        std::fprintf(fp, "P6\n%d %d\n255\n", w, h);
+        for (uint32_t v : px) {
+            unsigned char rgb[3] = {(unsigned char)(v & 255), (unsigned char)((v >> 8) & 255),
+                                    (unsigned char)((v >> 16) & 255)};
+            std::fwrite(rgb, 1, 3, fp);
+        }
+        std::fclose(fp);
+    }
+    return 0;
+}

@@ -1,0 +1,118 @@
+// rm_pass.hpp -- C++ host adapter over the rm.h C ABI that mirrors the SFML
+// surface the reference's main.cpp drives its ray-march pass through, so that
+// main.cpp:52-54,187-207 port one call for one call:
+//
+//   reference (SFML)                                   here
+//   sf::Shader shader;                                 rm::Shader shader(device);
+//   ShaderLoader::loadFromFile(f, sf::Shader::Fragment, rm::ShaderLoader::loadFromFile(f, rm::Shader::Fragment,
+//                              shader)  -> bool                                    shader) -> bool
+//   shader.setUniform("u_pos", sf::Vector3f)           shader.setUniform("u_pos", rm::Vec3{...})
+//   sf::RenderTexture t; t.create(w, h);               rm::RenderTexture t; t.create(w, h);
+//   t.draw(sprite, &shader);                           t.draw(shader);
+//   t.getTexture()                                     t.texture() (device RGBA32F) / t.copyToHost(...)
+//
+// Errors follow the reference: loadFromFile prints and returns false
+// (source/shader_loader.cpp:26-30); other calls return false and keep the
+// message in lastError().  Header-only; link with librm.so.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "rm.h"
+
+namespace rm {
+
+struct Vec2 { float x, y; };
+struct Vec3 { float x, y, z; };
+
+class Shader {
+public:
+    enum Type { Fragment };
+
+    explicit Shader(int device = 0) {
+        if (rm_create(&ctx_, device) != RM_OK) ctx_ = nullptr;
+    }
+    ~Shader() {
+        if (ctx_) rm_destroy(ctx_);
+    }
+    Shader(const Shader&) = delete;
+    Shader& operator=(const Shader&) = delete;
+
+    bool valid() const { return ctx_ != nullptr; }
+    rm_ctx* ctx() { return ctx_; }
+    std::string lastError() const { return ctx_ ? rm_last_error(ctx_) : "no HIP device"; }
+
+    bool setUniform(const char* name, float x) { return ctx_ && rm_set_uniform1f(ctx_, name, x) == RM_OK; }
+    bool setUniform(const char* name, Vec2 v) { return ctx_ && rm_set_uniform2f(ctx_, name, v.x, v.y) == RM_OK; }
+    bool setUniform(const char* name, Vec3 v) {
+        return ctx_ && rm_set_uniform3f(ctx_, name, v.x, v.y, v.z) == RM_OK;
+    }
+    // The reference's compile-time MAX_MARCHING_STEPS (common.frag:15) and the
+    // uncapped soft-shadow loop (common.frag:814) are run-time here.
+    bool setMarchSteps(int max_steps, int shadow_max_steps = 0) {
+        rm_params p;
+        if (!ctx_ || rm_get_params(ctx_, &p) != RM_OK) return false;
+        p.max_steps = max_steps;
+        p.shadow_max_steps = shadow_max_steps;
+        return rm_set_params(ctx_, &p) == RM_OK;
+    }
+
+private:
+    rm_ctx* ctx_ = nullptr;
+};
+
+struct ShaderLoader {
+    // source/shader_loader.h:11
+    static bool loadFromFile(const char* file_name, Shader::Type, Shader& out_shader) {
+        if (!out_shader.valid()) {
+            std::fprintf(stderr, "ShaderLoader: no HIP device\n");
+            return false;
+        }
+        return rm_load_scene(out_shader.ctx(), file_name) == RM_OK;  // prints its own message on failure
+    }
+};
+
+// A W x H RGBA32F render target resident in device memory (sf::RenderTexture).
+class RenderTexture {
+public:
+    ~RenderTexture() { release(); }
+    bool create(int w, int h) {
+        release();
+        w_ = w;
+        h_ = h;
+        return hipMalloc(&tex_, (size_t)w * h * 4 * sizeof(float)) == hipSuccess;
+    }
+    // RenderTarget::draw(sprite, &shader) with the full-screen sprite (main.cpp:199,205)
+    bool draw(Shader& shader, rm_stats* stats = nullptr) {
+        return tex_ && rm_render(shader.ctx(), w_, h_, tex_, stats) == RM_OK;
+    }
+    float* texture() { return tex_; }
+    int width() const { return w_; }
+    int height() const { return h_; }
+    // RGBA8 (the reference target's format), row 0 first (looks up).
+    bool copyToHostRGBA8(Shader& shader, std::vector<uint32_t>& out) {
+        out.resize((size_t)w_ * h_);
+        uint32_t* d = nullptr;
+        if (hipMalloc(&d, out.size() * sizeof(uint32_t)) != hipSuccess) return false;
+        bool ok = rm_pack_rgba8(shader.ctx(), (int64_t)out.size(), tex_, d) == RM_OK &&
+                  rm_synchronize(shader.ctx()) == RM_OK &&
+                  hipMemcpy(out.data(), d, out.size() * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess;
+        (void)hipFree(d);
+        return ok;
+    }
+
+private:
+    void release() {
+        if (tex_) (void)hipFree(tex_);
+        tex_ = nullptr;
+    }
+    float* tex_ = nullptr;
+    int w_ = 0, h_ = 0;
+};
+
+}  // namespace rm

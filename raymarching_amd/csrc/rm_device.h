@@ -110,6 +110,11 @@ __device__ __forceinline__ float menger(V3 p) {
     constexpr float INV[3] = {1.0f / 3.0f, 1.0f / 9.0f, 1.0f / 27.0f};
 #pragma unroll
     for (int m = 0; m < 3; m++) {
+        // Fold m yields c = (med3(r) - 1)/s with med3(r) <= 2, so c <= 1/s: once
+        // d >= 1/s the remaining folds cannot raise d (the `if (c > d)` of
+        // common.frag:671 never fires) and the result is exactly d.  Far from
+        // the sponge (most march and shadow steps) whole waves skip the folds.
+        if (d >= INV[m]) return d;
         float hx = p.x * SH[m], hy = p.y * SH[m], hz = p.z * SH[m];
         float ax = fmaf(2.0f, hx - floorf(hx), -1.0f);
         float ay = fmaf(2.0f, hy - floorf(hy), -1.0f);
