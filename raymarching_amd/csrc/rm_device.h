@@ -157,47 +157,48 @@ __device__ __forceinline__ V3 sponge_space(const FrameConst& F, V3 p) {
 }
 
 // sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4
+template <bool EXACT>
 __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& m) {
-    float h = div_const(fmaxf(k - fabsf(a - b), 0.0f), k, 1.0f / k);
+    float x = fmaxf(k - fabsf(a - b), 0.0f);
+    float h = EXACT ? div_const(x, k, 1.0f / k) : x * (1.0f / k);
     m = h * h * h * 0.5f;
     float s = m * k * (1.0f / 3.0f);
     return (a < b ? a : b) - s;
 }
 
+template <bool EXACT>
+__device__ __forceinline__ float len3(float x, float y, float z) {
+    float l2 = x * x + y * y + z * z;
+    return EXACT ? sqrtf(l2) : __builtin_amdgcn_sqrtf(l2);
+}
+
 // cube(vec4(c, r), p) (common.frag:589-593)
+template <bool EXACT>
 __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
     float qx = fabsf(p.x - c.x) - r, qy = fabsf(p.y - c.y) - r, qz = fabsf(p.z - c.z) - r;
-    float ex = fmaxf(qx, 0.0f), ey = fmaxf(qy, 0.0f), ez = fmaxf(qz, 0.0f);
-    return sqrtf(ex * ex + ey * ey + ez * ez) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f);
+    return len3<EXACT>(fmaxf(qx, 0.0f), fmaxf(qy, 0.0f), fmaxf(qz, 0.0f)) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f);
 }
 
-// Scene distances ("one ray-step" = one call).
-template <int SC>
-__device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p);
-
-template <>
-__device__ __forceinline__ float scene_dist<SCENE_S0>(const FrameConst&, V3 p) {
-    return length(p - v3(0.0f, 1.0f, -3.0f)) - 1.0f;
+// Scene distances ("one ray-step" = one call).  EXACT keeps the GLSL's
+// roundings (scene O's marches and normals, whose results feed the normal
+// hash); the fast form serves every other call.
+template <int SC, bool EXACT>
+__device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p) {
+    if constexpr (SC == SCENE_S0) {
+        return len3<EXACT>(p.x, p.y - 1.0f, p.z + 3.0f) - 1.0f;  // sphere(vec4(0,1,-3,1), p)
+    } else if constexpr (SC == SCENE_T) {
+        return menger<EXACT>(sponge_space<EXACT>(F, p));  // template.frag:41 (repaired)
+    } else {  // output_shader.frag:38-48
+        float d0 = menger<EXACT>(sponge_space<EXACT>(F, p));
+        float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
+        float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+        float d3 = p.y;
+        float m;
+        float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
+        float t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
+        return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
+    }
 }
-template <>
-__device__ __forceinline__ float scene_dist<SCENE_T>(const FrameConst& F, V3 p) {
-    return menger<false>(sponge_space<false>(F, p));  // template.frag:41 (repaired)
-}
-// output_shader.frag:38-48
-__device__ __forceinline__ float scene_dist_O(const FrameConst& F, V3 p) {
-    float d0 = menger<true>(sponge_space<true>(F, p));
-    float d1 = length(p - v3(3.0f, 2.0f, 3.0f)) - 1.0f;
-    float d2 = cube(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
-    float d3 = p.y;
-    float m;
-    float t1 = smin_cubic_d(d1, d2, 0.5f, m);
-    float t2 = smin_cubic_d(t1, d3, 0.5f, m);
-    return smin_cubic_d(d0, t2, 0.33f, m);
-}
-template <>
-__device__ __forceinline__ float scene_dist<SCENE_O>(const FrameConst& F, V3 p) { return scene_dist_O(F, p); }
-template <>
-__device__ __forceinline__ float scene_dist<SCENE_OG>(const FrameConst& F, V3 p) { return scene_dist_O(F, p); }
 
 // ------------------------------------------------------------- materials
 
@@ -250,16 +251,16 @@ __device__ __forceinline__ Mat scene_mat(const FrameConst& F, V3 p) {
     if constexpr (SC == SCENE_O || SC == SCENE_OG) {
         constexpr bool glass = SC == SCENE_OG;
         float d0 = menger<true>(sponge_space<true>(F, p));
-        float d1 = length(p - v3(3.0f, 2.0f, 3.0f)) - 1.0f;
-        float d2 = cube(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+        float d1 = len3<true>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
+        float d2 = cube<true>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
         float d3 = p.y;
         float m1, m2, m3;
-        float t1 = smin_cubic_d(d1, d2, 0.5f, m1);
+        float t1 = smin_cubic_d<true>(d1, d2, 0.5f, m1);
         Mat b = mat_blue(glass);
         Mat mt1 = smin_mat(d1, b, d2, b, m1);
-        float t2 = smin_cubic_d(t1, d3, 0.5f, m2);
+        float t2 = smin_cubic_d<true>(t1, d3, 0.5f, m2);
         Mat mt2 = smin_mat(t1, mt1, d3, floor_mat(p), m2);
-        (void)smin_cubic_d(d0, t2, 0.33f, m3);
+        (void)smin_cubic_d<true>(d0, t2, 0.33f, m3);
         return smin_mat(d0, mat_mirror(), t2, mt2, m3);
     } else {
         (void)F; (void)p;
@@ -270,17 +271,24 @@ __device__ __forceinline__ Mat scene_mat(const FrameConst& F, V3 p) {
 // ---------------------------------------------------------- post-colour
 
 // common.frag:1044-1051
+template <bool FAST>
+__device__ __forceinline__ float gpow(float x, float y) {
+    if constexpr (FAST) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+    else return powf(x, y);
+}
+template <bool FAST>
 __device__ __forceinline__ float tonemap1(float c, float e2) {
     float col = c * 2.0f / (1.0f + c);
-    col = powf(col, 0.4545f);
-    col = powf(col, e2);
+    col = gpow<FAST>(col, 0.4545f);
+    col = gpow<FAST>(col, e2);
     return col * 0.5f + 0.5f * col * col * (3.0f - 2.0f * col);
 }
 // tonemap -> contrast (common.frag:1067) -> vignette(.., 0.1) (:1072)
+template <bool FAST>
 __device__ __forceinline__ V3 post_colour(V3 c, float tcx, float tcy) {
-    V3 t = v3(tonemap1(c.x, 0.85f), tonemap1(c.y, 0.97f), tonemap1(c.z, 1.0f));
+    V3 t = v3(tonemap1<FAST>(c.x, 0.85f), tonemap1<FAST>(c.y, 0.97f), tonemap1<FAST>(c.z, 1.0f));
     t = v3(smoothstep(0.15f, 1.1f, t.x), smoothstep(0.15f, 1.1f, t.y), smoothstep(0.15f, 1.1f, t.z));
-    float v = 0.5f + 0.5f * powf(16.0f * tcx * tcy * (1.0f - tcx) * (1.0f - tcy), 0.1f);
+    float v = 0.5f + 0.5f * gpow<FAST>(16.0f * tcx * tcy * (1.0f - tcx) * (1.0f - tcy), 0.1f);
     return t * v;
 }
 

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void rm_render_direct(FrameConst F, float4* __
         V3 ro, rd;
         camera_ray(F, x, y, tcx, tcy, ro, rd);
         V3 c = render_pixel<SC>(F, ro, rd, cnt);
-        c = post_colour(c, tcx, tcy);
+        c = post_colour<FastMath<SC>::value>(c, tcx, tcy);
         out[(size_t)j * F.W + x] = make_float4(c.x, c.y, c.z, 1.0f);
     }
     if constexpr (COUNT) {

@@ -10,19 +10,57 @@
 
 namespace rm {
 
+// Scenes S0 and T use GLSL-precision hardware ops (v_rcp/v_sqrt/v_rsq and
+// pow = exp2(y*log2 x), as GPU GLSL compilers emit them); scene O keeps the
+// libm-accurate forms because its normal hash amplifies ulp differences.
+template <int SC>
+struct FastMath {
+    static constexpr bool value = SC == SCENE_T || SC == SCENE_S0;
+};
+template <int SC>
+__device__ __forceinline__ float mdiv(float a, float b) {
+    if constexpr (FastMath<SC>::value) return a * __builtin_amdgcn_rcpf(b);
+    else return a / b;
+}
+template <int SC>
+__device__ __forceinline__ float msqrt(float x) {
+    if constexpr (FastMath<SC>::value) return __builtin_amdgcn_sqrtf(x);
+    else return sqrtf(x);
+}
+template <int SC>
+__device__ __forceinline__ float mpow(float x, float y) {
+    if constexpr (FastMath<SC>::value) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+    else return powf(x, y);
+}
+// the scene distance for marches and normals (exact for scene O), and for
+// the AO / shadow / thickness probes, whose results are smooth in the distance
+template <int SC>
+__device__ __forceinline__ float dist_march(const FrameConst& F, V3 p) {
+    return scene_dist<SC, !FastMath<SC>::value>(F, p);
+}
+template <int SC>
+__device__ __forceinline__ float dist_probe(const FrameConst& F, V3 p) {
+    return scene_dist<SC, false>(F, p);
+}
+template <int SC>
+__device__ __forceinline__ V3 mnormalize(V3 a) {
+    if constexpr (FastMath<SC>::value) return a * __builtin_amdgcn_rsqf(dot(a, a));
+    else return normalize(a);
+}
+
 // common.frag:697-708 (tetrahedral gradient, h = 0.001)
 template <int SC>
 __device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, uint32_t& cnt) {
     const float h = 0.001f;
-    float d0 = scene_dist<SC>(F, p + v3(h, -h, -h));
-    float d1 = scene_dist<SC>(F, p + v3(-h, -h, h));
-    float d2 = scene_dist<SC>(F, p + v3(-h, h, -h));
-    float d3 = scene_dist<SC>(F, p + v3(h, h, h));
+    float d0 = dist_march<SC>(F, p + v3(h, -h, -h));
+    float d1 = dist_march<SC>(F, p + v3(-h, -h, h));
+    float d2 = dist_march<SC>(F, p + v3(-h, h, -h));
+    float d3 = dist_march<SC>(F, p + v3(h, h, h));
     cnt += 4;
     V3 g = v3(d0, -d0, -d0) + v3(-d1, -d1, d1);
     g = g + v3(-d2, d2, -d2);
     g = g + v3(d3, d3, d3);
-    return normalize(g);
+    return mnormalize<SC>(g);
 }
 
 // common.frag:879-901. Returns dist (depth on hit, -1 on miss, last SDF value
@@ -34,7 +72,7 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
     last_q = ro;
     for (int i = 0; i < F.max_steps; i++) {
         V3 q = ro + rd * depth;
-        res = scene_dist<SC>(F, q);
+        res = dist_march<SC>(F, q);
         cnt++;
         last_q = q;
         if (INSIDE) {  // castRayDI, common.frag:903-925
@@ -55,7 +93,7 @@ __device__ __forceinline__ V3 cast_ray(const FrameConst& F, V3 ro, V3 rd, uint32
     float depth = ZNEAR;
     V3 p = ro + rd * depth;
     for (int i = 0; i < F.max_steps; i++) {
-        float dist = scene_dist<SC>(F, p);
+        float dist = dist_march<SC>(F, p);
         cnt++;
         if (dist < 0.001f) return p;
         depth += dist;
@@ -74,12 +112,12 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
     int it = 0;
     for (float t = mint; t < maxt;) {
         if (F.shadow_max_steps > 0 && it++ >= F.shadow_max_steps) break;
-        float h = scene_dist<SC>(F, ro + rd * t);
+        float h = dist_probe<SC>(F, ro + rd * t);
         cnt++;
         if (h < 0.001f) return 0.0f;
-        float y = h * h / (2.0f * ph);
-        float d = sqrtf(h * h - y * y);
-        res = fminf(res, k * d / fmaxf(0.0f, t - y));
+        float y = mdiv<SC>(h * h, 2.0f * ph);
+        float d = msqrt<SC>(h * h - y * y);
+        res = fminf(res, mdiv<SC>(k * d, fmaxf(0.0f, t - y)));
         ph = h;
         t += h * 0.1f + 0.001f;
     }
@@ -93,7 +131,7 @@ __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, uint
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         V3 p = pos + (n * (float)(i + 1)) * 0.2f;
-        sum += (1.0f / (float)(1 << i)) * scene_dist<SC>(F, p);
+        sum += (1.0f / (float)(1 << i)) * dist_probe<SC>(F, p);
     }
     cnt += 4;
     // maxSum = sum_i 2^-i (i+1) 0.2, accumulated in f32 as the reference does
@@ -104,18 +142,22 @@ __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, uint
 }
 
 // common.frag:730-754 (N = the caller's normal)
+template <int SC>
 __device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 p, V3 eye, V3 lightPos, V3 N) {
-    V3 L = normalize(lightPos - p);
-    V3 V = normalize(eye - p);
-    V3 R = normalize(reflect(-L, N));
+    V3 L = mnormalize<SC>(lightPos - p);
+    V3 V = mnormalize<SC>(eye - p);
+    V3 R = mnormalize<SC>(reflect(-L, N));
     float dotLN = dot(L, N);
     float dotRV = dot(R, V);
     if (dotLN < 0.0f) return v3s(0.0f);
     if (dotRV < 0.0f) return k_d * dotLN;
-    return k_d * dotLN + k_s * powf(dotRV, alpha);
+    return k_d * dotLN + k_s * mpow<SC>(dotRV, alpha);
 }
 
-__device__ __forceinline__ V3 shadow_pow(float sha) { return v3(powf(sha, 1.0f), powf(sha, 1.2f), powf(sha, 1.5f)); }
+template <int SC>
+__device__ __forceinline__ V3 shadow_pow(float sha) {
+    return v3(mpow<SC>(sha, 1.0f), mpow<SC>(sha, 1.2f), mpow<SC>(sha, 1.5f));
+}
 
 // output_shader.frag:85-116
 template <int SC>
@@ -127,7 +169,7 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
         float sl = F.hash11[i];
         V3 rnd = normalize(hash33(nn + v3s(fi)) - v3s(0.5f));
         V3 dir = rnd - (nn * 2.0f) * fminf(0.0f, dot(rnd, nn));  // reflectVector (:70-73)
-        th += sl + scene_dist<SC>(F, pos + dir * sl);
+        th += sl + dist_probe<SC>(F, pos + dir * sl);
     }
     cnt += 32;
     return clamp01(th * 0.03125f);
@@ -143,7 +185,8 @@ __device__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V
     float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, length(Ld), cnt);
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
-    V3 shading = phong(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, p, ro, lightPos, phongN) * shadow_pow(sha);
+    V3 shading =
+        phong<SC>(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, p, ro, lightPos, phongN) * shadow_pow<SC>(sha);
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
     float th = thickness<SC>(F, p, n, cnt);
@@ -241,16 +284,19 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, uint32
     // getColorReflect (common.frag:991-1002); its dead nr normal is skipped
     V3 rdir = reflect(rd, n);
     V3 pr = cast_ray<SC>(F, p + rdir * 0.01f, rdir, cnt);
-    float c = clamp01(length(pr - p) / 3.0f);
+    float c = clamp01(length(pr - p) * (1.0f / 3.0f));
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
-    V3 lightDir = normalize(Ld);
+    float ld2 = dot(Ld, Ld);
+    V3 lightDir = Ld * __builtin_amdgcn_rsqf(ld2);
     float occ = ao_real<SC>(F, p, n, cnt);
-    float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, length(Ld), cnt);
+    float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
     float sky = clamp01(0.5f + 0.5f * n.y);
-    float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
-    float fre = powf(clamp01(1.0f + dot(n, rd)), 2.0f);
-    V3 shading = phong(v3(1.64f, 1.27f, 0.99f), v3(1.0f, 1.0f, 0.0f), 1280.0f, p, ro, lightPos, n) * shadow_pow(sha);
+    float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
+    float fre = clamp01(1.0f + dot(n, rd));
+    fre = fre * fre;  // pow(x, 2.0)
+    V3 shading =
+        phong<SC>(v3(1.64f, 1.27f, 0.99f), v3(1.0f, 1.0f, 0.0f), 1280.0f, p, ro, lightPos, n) * shadow_pow<SC>(sha);
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
     shading = shading + v3s(fre * occ);
@@ -265,7 +311,7 @@ __device__ __forceinline__ V3 render_S0(const FrameConst& F, V3 ro, V3 rd, uint3
     if (dist > 0.0f) {
         V3 p = ro + rd * dist;
         V3 n = normal_fast<SC>(F, p, cnt);
-        V3 lightDir = normalize(v3(20.0f, 50.0f, 0.0f) - p);
+        V3 lightDir = mnormalize<SC>(v3(20.0f, 50.0f, 0.0f) - p);
         return v3(0.2f, 0.02f, 0.02f) * (0.1f + clamp01(dot(n, lightDir)));
     }
     return background(ro, rd);
