@@ -203,9 +203,15 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
 
 rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out, rm_stats *stats) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
-    if (!out || W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
-        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard/pointer");
+    if (W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
     if ((long long)W * H > (1LL << 31)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: frame too large");
+    if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
+    if (rows_of_shard(H, band, nshards, shard) == 0) {  // more shards than bands: nothing to do
+        if (stats) *stats = rm_stats{0, 0, 0.0f, ctx->scene};
+        return RM_OK;
+    }
+    if (!out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: null output");
     RM_HIP(hipSetDevice(ctx->device));
     if (is_device_ptr(out)) return render_dev(ctx, W, H, band, nshards, shard, reinterpret_cast<float4 *>(out), stats);
     size_t bytes = (size_t)W * rows_of_shard(H, band, nshards, shard) * sizeof(float4);

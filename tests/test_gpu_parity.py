@@ -142,12 +142,14 @@ def test_ragged_sizes(R, W, H):
         check_evals(st, ev, tol=2e-2)
 
 
-def test_u_resolution_independent_of_target(R):
+def test_u_resolution_independent_of_target(torch_cuda):
     """uv uses u_resolution (output_shader.frag:390); gl_TexCoord uses the target."""
-    setup(R, "T", POSES["P0"], 128, res=(1600.0, 900.0))
-    img, _ = hip(R, 96, 96)
+    r = rm.Renderer(0)  # own context: u_resolution stays set on a context
+    setup(r, "T", POSES["P0"], 128, res=(1600.0, 900.0))
+    img, _ = hip(r, 96, 96)
     o, _ = ref("T", 96, 96, POSES["P0"], 128, res=(1600.0, 900.0))
     assert_parity("T", img, o)
+    r.close()
 
 
 # ------------------------------------------------------ sharding / frames
