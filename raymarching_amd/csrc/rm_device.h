@@ -100,11 +100,11 @@ __device__ __forceinline__ float div_const(float x, float b, float rb) {
 // the fast form fuses them (fma) and divides by s through a reciprocal.
 template <bool EXACT>
 __device__ __forceinline__ float menger(V3 p) {
-    float dx = fabsf(p.x) - 1.0f, dy = fabsf(p.y) - 1.0f, dz = fabsf(p.z) - 1.0f;
-    float mc = fmaxf(dx, fmaxf(dy, dz));
-    float ex = fmaxf(dx, 0.0f), ey = fmaxf(dy, 0.0f), ez = fmaxf(dz, 0.0f);
-    float l2 = ex * ex + ey * ey + ez * ez;
-    float d = fminf(mc, EXACT ? sqrtf(l2) : __builtin_amdgcn_sqrtf(l2));
+    // sdBox(p, vec3(1)) = min(mc, length(max(di, 0))) with mc = max(di)
+    // (common.frag:595-600) is exactly mc: if mc <= 0 the length is 0 >= mc;
+    // otherwise the rounded sum of squares is >= RN(mc*mc) and a correctly
+    // rounded sqrt of RN(mc*mc) is mc, so the length is >= mc.  No sqrt.
+    float d = fmaxf(fabsf(p.x) - 1.0f, fmaxf(fabsf(p.y) - 1.0f, fabsf(p.z) - 1.0f));
     constexpr float SH[3] = {0.5f, 1.5f, 4.5f};                      // s/2 before s *= 3
     constexpr float S3[3] = {3.0f, 9.0f, 27.0f};                     // s after s *= 3
     constexpr float INV[3] = {1.0f / 3.0f, 1.0f / 9.0f, 1.0f / 27.0f};

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""profiles/pmc_traffic.json from a tools/pmc_profile.sh summary.
+
+HBM bytes per launch of the render kernel = (2 * FETCH_SIZE + WRITE_SIZE) * 1024:
+FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads half the bytes of
+wide coalesced reads (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for
+16-B-per-lane stores (our float4 framebuffer writes).
+usage: make_traffic_json.py SUMMARY.json KEY [KERNEL_SUBSTR] [OUT]
+"""
+import json
+import os
+import sys
+
+summ, key = sys.argv[1], sys.argv[2]
+ksub = sys.argv[3] if len(sys.argv) > 3 else "rm_render_direct<1, false>"
+out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
+d = json.load(open(summ))
+k = [n for n in d if ksub in n][0]
+v = d[k]
+entry = {"kernel": k, "FETCH_SIZE_KiB": v["FETCH_SIZE"], "WRITE_SIZE_KiB": v["WRITE_SIZE"],
+         "hbm_bytes_per_launch": (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024,
+         "source": os.path.relpath(summ)}
+allj = json.load(open(out)) if os.path.exists(out) else {}
+allj[key] = entry
+json.dump(allj, open(out, "w"), indent=1)
+print(key, entry)
