@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--band", type=int, default=16)
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "wave"])
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(HERE, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary used for roofline.traffic (if it matches the workload)")
@@ -107,10 +109,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # (ranks > GPUs only in single-GPU gloo rehearsals)
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     W = args.size
     H = args.height or args.size
@@ -128,7 +135,8 @@ def main():
     r.set_params(count_evals=1)
     _, st = fr.render_local(stats=True)
     r.set_params(count_evals=0)
-    ev_rank = torch.tensor([st["evals"]], dtype=torch.float64, device=dev)
+    red_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    ev_rank = torch.tensor([st["evals"]], dtype=torch.float64, device=red_dev)
     ev_total = ev_rank.clone()
     if world > 1:
         dist.all_reduce(ev_total)
@@ -154,9 +162,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     kern = sum(a.elapsed_time(b) for a, b in zip(k0, k1)) / args.steps  # ms, this rank
-    kt = torch.tensor([kern], dtype=torch.float64, device=dev)
+    kt = torch.tensor([kern], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
@@ -169,7 +177,7 @@ def main():
         traffic = None
         try:
             pm = json.load(open(args.pmc))
-            key = f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}"
+            key = f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}" + ("" if world == 1 else f"_n{world}")
             traffic = pm.get(key, {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass

@@ -98,13 +98,17 @@ __device__ __forceinline__ float div_const(float x, float b, float rb) {
 //   min(max(rx,ry), max(ry,rz), max(rz,rx)) == med3(rx, ry, rz)
 // EXACT keeps the reference's roundings (separate 1 - 3|a|, division by s);
 // the fast form fuses them (fma) and divides by s through a reciprocal.
+//
+// sdBox(p, vec3(1)) = min(mc, length(max(di, 0))) with mc = max(di)
+// (common.frag:595-600) is exactly mc: if mc <= 0 the length is 0 >= mc;
+// otherwise the rounded sum of squares is >= RN(mc*mc) and a correctly rounded
+// sqrt of RN(mc*mc) is mc, so the length is >= mc.  No sqrt.
+__device__ __forceinline__ float sponge_box(V3 p) {
+    return fmaxf(fabsf(p.x) - 1.0f, fmaxf(fabsf(p.y) - 1.0f, fabsf(p.z) - 1.0f));
+}
+// the three folds, starting from the box term d; the result is >= d
 template <bool EXACT>
-__device__ __forceinline__ float menger(V3 p) {
-    // sdBox(p, vec3(1)) = min(mc, length(max(di, 0))) with mc = max(di)
-    // (common.frag:595-600) is exactly mc: if mc <= 0 the length is 0 >= mc;
-    // otherwise the rounded sum of squares is >= RN(mc*mc) and a correctly
-    // rounded sqrt of RN(mc*mc) is mc, so the length is >= mc.  No sqrt.
-    float d = fmaxf(fabsf(p.x) - 1.0f, fmaxf(fabsf(p.y) - 1.0f, fabsf(p.z) - 1.0f));
+__device__ __forceinline__ float sponge_folds(V3 p, float d) {
     constexpr float SH[3] = {0.5f, 1.5f, 4.5f};                      // s/2 before s *= 3
     constexpr float S3[3] = {3.0f, 9.0f, 27.0f};                     // s after s *= 3
     constexpr float INV[3] = {1.0f / 3.0f, 1.0f / 9.0f, 1.0f / 27.0f};
@@ -134,6 +138,10 @@ __device__ __forceinline__ float menger(V3 p) {
         d = fmaxf(d, c);  // if (c > d) d = c;
     }
     return d;
+}
+template <bool EXACT>
+__device__ __forceinline__ float menger(V3 p) {
+    return sponge_folds<EXACT>(p, sponge_box(p));
 }
 
 // transformR(p - vec3(0,3,0), vec3(180, 2t, 0)): row vector times rotationY
@@ -189,13 +197,19 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p) {
     } else if constexpr (SC == SCENE_T) {
         return menger<EXACT>(sponge_space<EXACT>(F, p));  // template.frag:41 (repaired)
     } else {  // output_shader.frag:38-48
-        float d0 = menger<EXACT>(sponge_space<EXACT>(F, p));
         float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
         float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
         float d3 = p.y;
         float m;
         float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
         float t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
+        // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width
+        // k = 0.33 (with a margin far above rounding), sminCubic's h is 0 and the
+        // result is exactly t2: the sponge's folds are not needed.
+        V3 q = sponge_space<EXACT>(F, p);
+        float mc = sponge_box(q);
+        if (mc >= t2 + 0.34f) return t2;
+        float d0 = sponge_folds<EXACT>(q, mc);
         return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
     }
 }

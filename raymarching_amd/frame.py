@@ -53,19 +53,29 @@ class ShardPlan:
 
 def gather_to_root(local, plan: ShardPlan, rank: int, group=None, out=None):
     """Gather each rank's packed rows (padded to rows_per_shard) into a
-    [nshards, rows_per_shard, ...] tensor on rank 0 (None elsewhere)."""
+    [nshards, rows_per_shard, ...] tensor on rank 0 (None elsewhere).
+
+    With the "nccl" backend (RCCL on ROCm) device buffers go over xGMI
+    directly.  The "gloo" backend (CPU tests, and single-GPU rehearsals of the
+    multi-rank path) moves host memory, so device buffers are staged.
+    """
     import torch
     import torch.distributed as dist
 
     rps = plan.rows_per_shard
     if local.shape[0] != rps:
         raise ValueError(f"local band buffer must have rows_per_shard={rps} rows, has {local.shape[0]}")
+    staged = local.is_cuda and dist.get_backend(group) == "gloo"
+    src = local.cpu() if staged else local
     if rank == 0:
         if out is None:
             out = torch.empty((plan.nshards,) + tuple(local.shape), dtype=local.dtype, device=local.device)
-        dist.gather(local, gather_list=list(out.unbind(0)), dst=0, group=group)
+        dst = torch.empty(out.shape, dtype=out.dtype) if staged else out
+        dist.gather(src, gather_list=list(dst.unbind(0)), dst=0, group=group)
+        if staged:
+            out.copy_(dst)
         return out
-    dist.gather(local, gather_list=None, dst=0, group=group)
+    dist.gather(src, gather_list=None, dst=0, group=group)
     return None
 
 
