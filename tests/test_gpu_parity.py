@@ -330,3 +330,26 @@ def test_c3_4096_properties(R, torch_cuda):
 
 def test_c5_8192_scene_O(R, torch_cuda):
     strided_parity(R, "O", 8192, 8192, POSES["P0"], 512, 1024)
+
+
+def test_headless_cpp_host_app(tmp_path, torch_cuda):
+    """apps/raymarch_headless (main.cpp's frame loop over include/rm_pass.hpp):
+    the scripted camera walk ends where main.cpp:153-171 puts it, and the last
+    frame matches the oracle at that pose (RGBA8, time frozen at 0)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(__file__)), "apps", "raymarch_headless")
+    ppm = tmp_path / "f.ppm"
+    out = subprocess.run([exe, "--scene", "template.frag", "--w", "96", "--h", "54", "--frames", "6", "--script",
+                          "WWDDU.", "--time-freeze", "--ppm", str(ppm)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    # W,W,D,D,Up then idle with the mouse centred: x += 0.2, y += 0.1, z -= 0.2
+    np.testing.assert_allclose(info["pos"], [2.2, 3.1, 2.8], atol=1e-4)
+    data = ppm.read_bytes()
+    hdr_end = data.index(b"255\n") + 4
+    img = np.frombuffer(data[hdr_end:], np.uint8).reshape(54, 96, 3).astype(np.float32) / 255.0
+    pos = [np.float32(v) for v in info["pos"]]
+    o, _ = oracle.render("T", 96, 54, pos=pos, mouse=(0.0, 0.0), time=0.0, max_steps=128, res=(96.0, 54.0))
+    ref8 = np.clip(np.rint(np.clip(o[..., :3], 0, 1) * 255.0), 0, 255) / 255.0
+    d = np.abs(img - ref8).max(-1)
+    assert np.mean(d <= 2.0 / 255.0) >= 0.99, float(np.mean(d <= 2.0 / 255.0))
