@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--max-steps", type=int, default=256)
     ap.add_argument("--pose", default="P0")
     ap.add_argument("--band", type=int, default=16)
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="pipeline chunks per frame for N > 1 (render k+1 while gathering k); default 1 at N=1, 4 else")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "wave"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -129,7 +131,8 @@ def main():
     r.set_params(max_steps=args.max_steps, shadow_max_steps=0, kernel=args.kernel)
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream)
-    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt)
+    chunks = args.chunks if args.chunks is not None else (1 if world == 1 else 4)
+    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks)
 
     # instrumented run: ray-steps of this rank's rows, summed over ranks
     r.set_params(count_evals=1)
@@ -149,21 +152,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    k0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    k1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    nch = len(fr.cuts) - 1
+    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nch)]
+           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        k0[i].record(stream)
-        fr.render_local()
-        k1[i].record(stream)
-        fr.finish()
+        fr.render(events=evs[i])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-    kern = sum(a.elapsed_time(b) for a, b in zip(k0, k1)) / args.steps  # ms, this rank
+    live = [c for c in range(nch) if min(fr.cuts[c + 1], fr.nmine) > fr.cuts[c]]  # chunks with rows here
+    kern = sum(evs[i][c][0].elapsed_time(evs[i][c][1]) for i in range(args.steps) for c in live) / args.steps
     kt = torch.tensor([kern], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -200,7 +202,7 @@ def main():
                             f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
                             f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0",
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
-                "band": args.band, "fmt": args.fmt, "kernel": args.kernel,
+                "band": args.band, "fmt": args.fmt, "kernel": args.kernel, "chunks": chunks,
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
             },
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max,

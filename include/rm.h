@@ -103,6 +103,13 @@ rm_status rm_render(rm_ctx *ctx, int W, int H, float *out, rm_stats *stats);
 rm_status rm_render_band(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out,
                          rm_stats *stats);
 
+/* A sub-range of rm_render_band: the shard's packed rows [row_begin,
+ * row_begin + row_count) into `out` (row_count rows of W float4).  Lets a
+ * caller pipeline a shard in chunks (render chunk k+1 while chunk k is
+ * gathered). */
+rm_status rm_render_rows(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
+                         float *out, rm_stats *stats);
+
 /* Number of frame rows shard `shard` owns. */
 rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows);
 

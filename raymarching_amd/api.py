@@ -128,6 +128,14 @@ class Renderer:
                                    ctypes.byref(s) if stats else None), self._ctx)
         return (out, s.as_dict()) if stats else out
 
+    def render_rows(self, W, H, band, nshards, shard, row_begin, row_count, out, stats=False):
+        """Packed rows [row_begin, row_begin + row_count) of a shard into `out`."""
+        _check_out(out, row_count * W * 4)
+        s = RmStats()
+        check(lib().rm_render_rows(self._ctx, int(W), int(H), int(band), int(nshards), int(shard), int(row_begin),
+                                   int(row_count), self._ptr(out), ctypes.byref(s) if stats else None), self._ctx)
+        return (out, s.as_dict()) if stats else out
+
     def deinterleave(self, W, H, band, nshards, rows_per_shard, gathered, out=None):
         """gathered: [nshards, rows_per_shard, W, 4] f32 or [nshards, rows_per_shard, W] RGBA8 words."""
         torch = _torch()

@@ -176,15 +176,16 @@ int pick_kernel(const rm_ctx *c) {
     return rm::has_wave_kernel_host(c->scene) ? rm::KERNEL_WAVE : rm::KERNEL_DIRECT;
 }
 
-// the pass itself: device output, optional stats (synchronous when given)
-rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float4 *out, rm_stats *stats) {
-    if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
-    int nrows = rows_of_shard(H, band, nshards, shard);
-    FrameConst F = frame_const(ctx, W, H, band, nshards, shard, nrows);
-    bool count = ctx->params.count_evals != 0;
-    if (count) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, sizeof(unsigned long long), ctx->stream));
+// the pass over packed rows [row0, row0 + count) of a shard: device output,
+// optional stats (synchronous when given)
+rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, float4 *out,
+                     rm_stats *stats) {
+    FrameConst F = frame_const(ctx, W, H, band, nshards, shard, count);
+    F.row0 = row0;
+    bool cnt = ctx->params.count_evals != 0;
+    if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, sizeof(unsigned long long), ctx->stream));
     if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-    hipError_t e = rm::launch_render(ctx->scene, F, out, count ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
+    hipError_t e = rm::launch_render(ctx->scene, F, out, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) {
         RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
@@ -192,32 +193,39 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         float ms = 0.0f;
         RM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
         unsigned long long ev = 0;
-        if (count) RM_HIP(hipMemcpy(&ev, ctx->d_evals, sizeof(ev), hipMemcpyDeviceToHost));
+        if (cnt) RM_HIP(hipMemcpy(&ev, ctx->d_evals, sizeof(ev), hipMemcpyDeviceToHost));
         stats->evals = ev;
-        stats->pixels = (uint64_t)W * (uint64_t)nrows;
+        stats->pixels = (uint64_t)W * (uint64_t)count;
         stats->kernel_ms = ms;
         stats->scene = ctx->scene;
     }
     return RM_OK;
 }
 
-rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out, rm_stats *stats) {
+// row_count < 0: every packed row from row_begin on
+rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
+                     float *out, rm_stats *stats) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
     if ((long long)W * H > (1LL << 31)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: frame too large");
     if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
-    if (rows_of_shard(H, band, nshards, shard) == 0) {  // more shards than bands: nothing to do
+    int n = rows_of_shard(H, band, nshards, shard);
+    if (row_count < 0) row_count = n - row_begin;
+    if (row_begin < 0 || row_count < 0 || row_begin + row_count > n)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: packed row range outside the shard");
+    if (row_count == 0) {  // e.g. more shards than bands: nothing to do
         if (stats) *stats = rm_stats{0, 0, 0.0f, ctx->scene};
         return RM_OK;
     }
     if (!out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: null output");
     RM_HIP(hipSetDevice(ctx->device));
-    if (is_device_ptr(out)) return render_dev(ctx, W, H, band, nshards, shard, reinterpret_cast<float4 *>(out), stats);
-    size_t bytes = (size_t)W * rows_of_shard(H, band, nshards, shard) * sizeof(float4);
+    if (is_device_ptr(out))
+        return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, reinterpret_cast<float4 *>(out), stats);
+    size_t bytes = (size_t)W * row_count * sizeof(float4);
     rm_status s = ensure_staging(ctx, bytes);
     if (s != RM_OK) return s;
-    s = render_dev(ctx, W, H, band, nshards, shard, ctx->staging, stats);
+    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, ctx->staging, stats);
     if (s != RM_OK) return s;
     RM_HIP(hipMemcpyAsync(out, ctx->staging, bytes, hipMemcpyDeviceToHost, ctx->stream));
     RM_HIP(hipStreamSynchronize(ctx->stream));
@@ -342,11 +350,17 @@ rm_status rm_synchronize(rm_ctx *ctx) {
 }
 
 rm_status rm_render(rm_ctx *ctx, int W, int H, float *out, rm_stats *stats) {
-    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, out, stats);
+    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, out, stats);
 }
 
 rm_status rm_render_band(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out, rm_stats *stats) {
-    return render_any(ctx, W, H, band, nshards, shard, out, stats);
+    return render_any(ctx, W, H, band, nshards, shard, 0, -1, out, stats);
+}
+
+rm_status rm_render_rows(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
+                         float *out, rm_stats *stats) {
+    if (row_count < 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rows: negative row_count");
+    return render_any(ctx, W, H, band, nshards, shard, row_begin, row_count, out, stats);
 }
 
 rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows) {
@@ -400,6 +414,8 @@ rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t 
 rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (!out || W <= 0 || H <= 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rgba8: bad arguments");
+    if ((long long)W * H > (1LL << 31)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: frame too large");
+    if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
     RM_HIP(hipSetDevice(ctx->device));
     size_t npx = (size_t)W * H;
     size_t fbytes = npx * sizeof(float4), bbytes = npx * sizeof(uint32_t);
@@ -407,7 +423,7 @@ rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *st
     bool dev_out = is_device_ptr(out);
     rm_status s = ensure_staging(ctx, fbytes + (dev_out ? 0 : bbytes));
     if (s != RM_OK) return s;
-    s = render_dev(ctx, W, H, H, 1, 0, ctx->staging, stats);
+    s = render_dev(ctx, W, H, H, 1, 0, 0, H, ctx->staging, stats);
     if (s != RM_OK) return s;
     uint32_t *dst = dev_out ? out : reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(ctx->staging) + fbytes);
     hipError_t e = rm::launch_pack_rgba8(ctx->staging, dst, npx, ctx->stream);

@@ -37,7 +37,8 @@ struct FrameConst {
                                    // rotationZ(-0) is the exact identity and is skipped
     int W, H;                      // target size (gl_TexCoord = ((x+.5)/W, (y+.5)/H))
     int band, nshards, shard;      // row y is rendered iff (y / band) % nshards == shard
-    int nrows;                     // rows of this shard (packed in increasing y)
+    int nrows;                     // packed rows rendered by this launch
+    int row0;                      // first packed row of the shard this launch renders
     int max_steps;                 // MAX_MARCHING_STEPS (common.frag:15), run-time
     int shadow_max_steps;          // 0 = unbounded, as softshadow2 (common.frag:814)
     float hash11[32];              // Hash11(i), i = 0..31 (output_shader.frag:54-59,102)

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void rm_render_direct(FrameConst F, float4* __
     const int j = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
     uint32_t cnt = 0;
     if (x < F.W && j < F.nrows) {
-        const int y = shard_row(F, j);
+        const int y = shard_row(F, F.row0 + j);
         float tcx, tcy;
         V3 ro, rd;
         camera_ray(F, x, y, tcx, tcy, ro, rd);

@@ -86,9 +86,14 @@ class DistributedFrame:
     de-interleaves the frame; everything is asynchronous on the current
     stream.  ``fmt`` is "rgba8" (the displayed RenderTexture format, 4 B/px on
     the wire) or "float4" (full gl_FragColor, 16 B/px, used by parity tests).
+
+    ``chunks`` > 1 pipelines a frame: the packed rows are cut into that many
+    row ranges (the same cuts on every rank, so gathers line up); chunk k+1 is
+    rendered on the compute stream while chunk k's gather (async, on RCCL's
+    stream) moves over xGMI, leaving only the last chunk's transfer exposed.
     """
 
-    def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None):
+    def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None, chunks=1):
         import torch
 
         self.r, self.rank, self.world, self.fmt, self.group = renderer, rank, world, fmt, group
@@ -96,6 +101,9 @@ class DistributedFrame:
         self.plan = ShardPlan(W, H, band if world > 1 else H, world)
         dev = torch.device(f"cuda:{renderer.device}")
         rps = self.plan.rows_per_shard
+        self.nmine = self.plan.count(rank)
+        chunks = max(1, min(int(chunks), rps))
+        self.cuts = [round(c * rps / chunks) for c in range(chunks + 1)]
         self.local = torch.empty((rps, W, 4), dtype=torch.float32, device=dev)
         self.local8 = torch.empty((rps, W), dtype=torch.int32, device=dev) if fmt == "rgba8" else None
         wire = self.local8 if fmt == "rgba8" else self.local
@@ -109,24 +117,43 @@ class DistributedFrame:
         else:
             self.frame = None
 
-    def render_local(self, stats=False):
+    def _render_chunk(self, c, events=None):
         p = self.plan
-        return self.r.render_band(p.W, p.H, p.band, p.nshards, self.rank, out=self.local, stats=stats)
-
-    def finish(self):
-        """Everything of a frame after the render kernel: pack, gather, de-interleave."""
-        p = self.plan
-        wire = self.local
+        j0, j1 = self.cuts[c], min(self.cuts[c + 1], self.nmine)
+        if j1 <= j0:
+            return
+        if events is not None:
+            events[0].record()
+        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, self.local[j0:j1])
+        if events is not None:
+            events[1].record()
         if self.fmt == "rgba8":
-            self.r.pack_rgba8(self.local, out=self.local8)
-            wire = self.local8
-        if self.world == 1:
-            return self.frame
-        g = gather_to_root(wire, p, self.rank, group=self.group, out=self.gathered)
-        if self.rank == 0:
-            self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, g, out=self.frame)
-        return self.frame
+            self.r.pack_rgba8(self.local[j0:j1], out=self.local8[j0:j1])
 
-    def render(self):
-        self.render_local()
-        return self.finish()
+    def render_local(self, stats=False):
+        """This rank's rows only (no gather); stats: one synchronous launch."""
+        p = self.plan
+        return self.r.render_band(p.W, p.H, p.band, p.nshards, self.rank, out=self.local[: self.nmine], stats=stats)
+
+    def render(self, events=None):
+        """One frame.  events: optional list of (start, end) torch.cuda.Event
+        pairs, one per chunk, recorded around the render kernels."""
+        import torch.distributed as dist
+
+        p = self.plan
+        wire = self.local8 if self.fmt == "rgba8" else self.local
+        pipelined = self.world > 1 and dist.get_backend(self.group) != "gloo"
+        works = []
+        for c in range(len(self.cuts) - 1):
+            self._render_chunk(c, None if events is None else events[c])
+            if pipelined:
+                j0, j1 = self.cuts[c], self.cuts[c + 1]
+                glist = [self.gathered[r, j0:j1] for r in range(self.world)] if self.rank == 0 else None
+                works.append(dist.gather(wire[j0:j1], gather_list=glist, dst=0, group=self.group, async_op=True))
+        if self.world > 1 and not pipelined:  # gloo: one host-staged gather
+            gather_to_root(wire, p, self.rank, group=self.group, out=self.gathered)
+        for w in works:
+            w.wait()
+        if self.world > 1 and self.rank == 0:
+            self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered, out=self.frame)
+        return self.frame

@@ -353,3 +353,24 @@ def test_headless_cpp_host_app(tmp_path, torch_cuda):
     ref8 = np.clip(np.rint(np.clip(o[..., :3], 0, 1) * 255.0), 0, 255) / 255.0
     d = np.abs(img - ref8).max(-1)
     assert np.mean(d <= 2.0 / 255.0) >= 0.99, float(np.mean(d <= 2.0 / 255.0))
+
+
+def test_render_rows_chunks_and_frame_pipeline(R, torch_cuda):
+    """rm_render_rows sub-ranges reassemble the band exactly; the chunked
+    single-rank DistributedFrame equals rm_render_rgba8."""
+    torch = torch_cuda
+    from raymarching_amd.frame import DistributedFrame
+    setup(R, "T", POSES["P6"], 128)
+    R.set_params(count_evals=0)
+    W, H, band, n, s = 72, 61, 5, 3, 1
+    full = R.render_band(W, H, band, n, s)
+    cnt = full.shape[0]
+    part = torch.empty_like(full)
+    for j0, j1 in ((0, 7), (7, 8), (8, cnt)):
+        R.render_rows(W, H, band, n, s, j0, j1 - j0, part[j0:j1])
+    assert torch.equal(part, full)
+    with pytest.raises(rm.RmError):
+        R.render_rows(W, H, band, n, s, cnt - 1, 2, part)
+    fr = DistributedFrame(R, 80, 48, 16, 0, 1, fmt="rgba8", chunks=5)
+    frame = fr.render()
+    assert torch.equal(frame, R.render_rgba8(80, 48))
