@@ -129,6 +129,12 @@ rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t 
 /* rm_render + rm_pack_rgba8 into a W*H uint32 target (device or host). */
 rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats);
 
+/* The reference's FXAA post pass (post.frag:16-61, :135-144) over an RGBA8
+ * frame: in/out W*H RGBA8 words (device, distinct), sampled as the reference's
+ * RenderTexture is (nearest, clamp to edge), u_resolution = (W, H).  Like
+ * post.frag, the output is the input flipped vertically. */
+rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
+
 /* Message of the last failing call on ctx ("" if none). */
 const char *rm_last_error(rm_ctx *ctx);
 const char *rm_status_string(rm_status status);

@@ -74,6 +74,8 @@ def lib(fast: bool = False) -> ctypes.CDLL:
                       ("oracle_smin_cubic", 3), ("oracle_hash11", 1)):
             getattr(L, fn).argtypes = [ctypes.c_float] * n
             getattr(L, fn).restype = ctypes.c_float
+        L.oracle_fxaa.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_fxaa.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         L.oracle_num_threads.restype = ctypes.c_int
         _LIBS[name] = L
@@ -134,3 +136,15 @@ def normal(scene: str, pts, **kw):
     lib().oracle_normal(SCENES[scene], ctypes.byref(u), _p(pts, ctypes.c_float), len(pts),
                         _p(out, ctypes.c_float))
     return out
+
+
+def fxaa(img_u32):
+    """post.frag FXAA over an [H, W] RGBA8 image -> (RGBA8 [H, W], float [H, W, 4])."""
+    img = np.ascontiguousarray(img_u32, np.uint32)
+    H, W = img.shape
+    out = np.zeros((H, W), np.uint32)
+    outf = np.zeros((H, W, 4), np.float32)
+    rc = lib().oracle_fxaa(W, H, img.ctypes.data, out.ctypes.data, outf.ctypes.data)
+    if rc:
+        raise ValueError("oracle_fxaa failed")
+    return out, outf

@@ -831,3 +831,87 @@ float oracle_smin_cubic(float a, float b, float k) {
     return sminCubic(&ra, &rb, k).dist;
 }
 float oracle_hash11(float p) { return Hash11(p); }
+
+/* ------------------------------------------------ post.frag FXAA pass */
+
+/* The FXAA pass (post.frag:16-61, main :135-144) as the reference runs it on
+ * its RGBA8 render target: texture() with the sampler state SFML leaves on an
+ * sf::RenderTexture (no setSmooth: GL_NEAREST; not repeated: CLAMP_TO_EDGE),
+ * u_resolution = (W, H) (main.cpp:58), unorm8 -> float c/255 on fetch and
+ * float -> unorm8 round-to-nearest on store.  Images are row 0 first, as the
+ * ray-march output. */
+typedef struct { float r, g, b, a; } rgba;
+#ifndef UNORM_K
+#define UNORM_K (1.0f / 255.0f)
+#endif
+
+static rgba tex_nearest(const uint32_t *img, int W, int H, vec2 uv) {
+    int x = (int)floorf(uv.x * (float)W);
+    int y = (int)floorf(uv.y * (float)H);
+    x = x < 0 ? 0 : (x >= W ? W - 1 : x);
+    y = y < 0 ? 0 : (y >= H ? H - 1 : y);
+    uint32_t v = img[(size_t)y * W + x];
+    const float k = UNORM_K;
+    rgba c = {(float)(v & 255u) * k, (float)((v >> 8) & 255u) * k, (float)((v >> 16) & 255u) * k,
+              (float)(v >> 24) * k};
+    return c;
+}
+
+static vec3 rgb_of(rgba c) { return v3(c.r, c.g, c.b); }
+static vec2 v2(float x, float y) { vec2 r = {x, y}; return r; }
+
+/* post.frag:16-61 */
+static rgba fxaa(const uint32_t *tex, int W, int H, vec2 fragCoord, vec2 resolution) {
+    const float FXAA_REDUCE_MIN = 1.0f / 128.0f, FXAA_REDUCE_MUL = 1.0f / 8.0f, FXAA_SPAN_MAX = 8.0f;
+    vec2 iv = v2(1.0f / resolution.x, 1.0f / resolution.y);
+    vec3 rgbNW = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + -1.0f * iv.x, fragCoord.y + -1.0f * iv.y)));
+    vec3 rgbNE = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + 1.0f * iv.x, fragCoord.y + -1.0f * iv.y)));
+    vec3 rgbSW = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + -1.0f * iv.x, fragCoord.y + 1.0f * iv.y)));
+    vec3 rgbSE = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + 1.0f * iv.x, fragCoord.y + 1.0f * iv.y)));
+    rgba texColor = tex_nearest(tex, W, H, fragCoord);
+    vec3 rgbM = rgb_of(texColor);
+    vec3 luma = v3(0.299f, 0.587f, 0.114f);
+    float lumaNW = dot3(rgbNW, luma), lumaNE = dot3(rgbNE, luma), lumaSW = dot3(rgbSW, luma);
+    float lumaSE = dot3(rgbSE, luma), lumaM = dot3(rgbM, luma);
+    float lumaMin = gmin(lumaM, gmin(gmin(lumaNW, lumaNE), gmin(lumaSW, lumaSE)));
+    float lumaMax = gmax(lumaM, gmax(gmax(lumaNW, lumaNE), gmax(lumaSW, lumaSE)));
+    vec2 dir = v2(-((lumaNW + lumaNE) - (lumaSW + lumaSE)), ((lumaNW + lumaSW) - (lumaNE + lumaSE)));
+    float dirReduce = gmax((lumaNW + lumaNE + lumaSW + lumaSE) * (0.25f * FXAA_REDUCE_MUL), FXAA_REDUCE_MIN);
+    float rcpDirMin = 1.0f / (gmin(fabsf(dir.x), fabsf(dir.y)) + dirReduce);
+    dir = v2(gmin(FXAA_SPAN_MAX, gmax(-FXAA_SPAN_MAX, dir.x * rcpDirMin)) * iv.x,
+             gmin(FXAA_SPAN_MAX, gmax(-FXAA_SPAN_MAX, dir.y * rcpDirMin)) * iv.y);
+    const float k1 = 1.0f / 3.0f - 0.5f, k2 = 2.0f / 3.0f - 0.5f;
+    vec3 s1 = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + dir.x * k1, fragCoord.y + dir.y * k1)));
+    vec3 s2 = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + dir.x * k2, fragCoord.y + dir.y * k2)));
+    vec3 rgbA = muls(add(s1, s2), 0.5f);
+    vec3 s3 = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + dir.x * -0.5f, fragCoord.y + dir.y * -0.5f)));
+    vec3 s4 = rgb_of(tex_nearest(tex, W, H, v2(fragCoord.x + dir.x * 0.5f, fragCoord.y + dir.y * 0.5f)));
+    vec3 rgbB = add(muls(rgbA, 0.5f), muls(add(s3, s4), 0.25f));
+    float lumaB = dot3(rgbB, luma);
+    rgba color;
+    vec3 c = (lumaB < lumaMin || lumaB > lumaMax) ? rgbA : rgbB;
+    color.r = c.x; color.g = c.y; color.b = c.z; color.a = texColor.a;
+    return color;
+}
+
+static uint32_t unorm8(float c) {
+    c = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
+    if (c != c) c = 0.0f;
+    return (uint32_t)lrintf(c * 255.0f);
+}
+
+/* post.frag:135-144: uv = (tc.x, 1 - tc.y); out = fxaa(u_main_tex, uv, res).
+ * out: RGBA8 words (may be NULL); out_f32: the float gl_FragColor (may be NULL). */
+int oracle_fxaa(int W, int H, const uint32_t *in, uint32_t *out, float *out_f32) {
+    if (!in || W <= 0 || H <= 0) return 1;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            vec2 tc = v2(((float)x + 0.5f) / (float)W, ((float)y + 0.5f) / (float)H);
+            rgba c = fxaa(in, W, H, v2(tc.x, 1.0f - tc.y), v2((float)W, (float)H));
+            size_t i = (size_t)y * W + x;
+            if (out) out[i] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | (unorm8(c.a) << 24);
+            if (out_f32) { out_f32[4 * i] = c.r; out_f32[4 * i + 1] = c.g; out_f32[4 * i + 2] = c.b; out_f32[4 * i + 3] = c.a; }
+        }
+    return 0;
+}

@@ -20,7 +20,7 @@ STATUS = {0: "RM_OK", 1: "RM_ERR_INVALID_ARGUMENT", 2: "RM_ERR_FILE", 3: "RM_ERR
 EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_set_uniform2f",
            "rm_set_uniform3f", "rm_set_params", "rm_get_params", "rm_set_stream", "rm_synchronize",
            "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8", "rm_pack_rgba8",
-           "rm_render_rgba8", "rm_last_error", "rm_status_string")
+           "rm_render_rgba8", "rm_fxaa", "rm_last_error", "rm_status_string")
 
 
 class RmParams(ctypes.Structure):
@@ -83,6 +83,7 @@ def lib() -> ctypes.CDLL:
         "rm_deinterleave_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_pack_rgba8": ([vp, c.c_int64, vp, vp], c.c_int),
         "rm_render_rgba8": ([vp, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
+        "rm_fxaa": ([vp, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_last_error": ([vp], cp),
         "rm_status_string": ([c.c_int], cp),
     }

@@ -160,6 +160,15 @@ class Renderer:
         check(lib().rm_pack_rgba8(self._ctx, npx, self._ptr(frame), self._ptr(out)), self._ctx)
         return out
 
+    def fxaa(self, frame8, out=None):
+        """post.frag's FXAA over an [H, W] RGBA8 (int32 words) device frame."""
+        torch = _torch()
+        H, W = frame8.shape
+        if out is None:
+            out = torch.empty_like(frame8)
+        check(lib().rm_fxaa(self._ctx, W, H, self._ptr(frame8), self._ptr(out)), self._ctx)
+        return out
+
     def render_rgba8(self, W, H, out=None, stats=False):
         torch = _torch()
         if out is None:

@@ -411,6 +411,17 @@ rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t 
     return RM_OK;
 }
 
+rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!in || !out || W <= 0 || H <= 0 || in == out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_fxaa: bad arguments");
+    if (!is_device_ptr(in) || !is_device_ptr(out))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_fxaa: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_fxaa(in, out, W, H, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "fxaa launch");
+    return RM_OK;
+}
+
 rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (!out || W <= 0 || H <= 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rgba8: bad arguments");

@@ -18,5 +18,6 @@ hipError_t launch_deinterleave_u32(const uint32_t* gathered, uint32_t* out, int 
                                    int rows_per_shard, hipStream_t s);
 hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStream_t s);
 bool has_wave_kernel_host(int scene);
+hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 
 }  // namespace rm

@@ -338,6 +338,76 @@ class GL:
         return buf[::-1].copy()  # GL rows bottom-up -> row 0 = tc.y 0.5/H
 
 
+    def post(self, prog, img_u32, res):
+        """Run a post pass reading `img_u32` (H x W RGBA8 words, row 0 first)
+        as u_main_tex with the sampler state of an sf::RenderTexture that was
+        never setSmooth()ed or setRepeated(): NEAREST, CLAMP_TO_EDGE; render
+        into an RGBA8 target and read the bytes back (row 0 = tc.y 0.5/H)."""
+        gl = self.gl
+        H, W = img_u32.shape
+        src = ctypes.c_uint()
+        gl.glGenTextures(1, ctypes.byref(src))
+        gl.glActiveTexture(0x84C0)
+        gl.glBindTexture(0x0DE1, src)
+        for pname, val in ((0x2801, 0x2600), (0x2800, 0x2600), (0x2802, 0x812F), (0x2803, 0x812F)):
+            gl.glTexParameteri(0x0DE1, pname, val)  # MIN/MAG NEAREST, WRAP_S/T CLAMP_TO_EDGE
+        data = np.ascontiguousarray(img_u32, np.uint32)
+        gl.glTexImage2D(0x0DE1, 0, 0x8058, W, H, 0, 0x1908, 0x1401, data.ctypes.data_as(ctypes.c_void_p))  # RGBA8
+        dst, fbo = ctypes.c_uint(), ctypes.c_uint()
+        gl.glGenTextures(1, ctypes.byref(dst))
+        gl.glBindTexture(0x0DE1, dst)
+        gl.glTexStorage2D(0x0DE1, 1, 0x8058, W, H)
+        gl.glGenFramebuffers(1, ctypes.byref(fbo))
+        gl.glBindFramebuffer(0x8D40, fbo)
+        gl.glFramebufferTexture2D(0x8D40, 0x8CE0, 0x0DE1, dst, 0)
+        assert gl.glCheckFramebufferStatus(0x8D40) == 0x8CD5
+        gl.glBindTexture(0x0DE1, src)
+        gl.glViewport(0, 0, W, H)
+        gl.glUseProgram(prog)
+        gl.glUniform2f(gl.glGetUniformLocation(prog, b"u_resolution"), float(res[0]), float(res[1]))
+        gl.glUniform1i(gl.glGetUniformLocation(prog, b"u_main_tex"), 0)
+        gl.glDrawArrays(0x0004, 0, 3)
+        gl.glFinish()
+        out = np.zeros((H, W), np.uint32)
+        gl.glReadPixels(0, 0, W, H, 0x1908, 0x1401, out.ctypes.data_as(ctypes.c_void_p))
+        assert gl.glGetError() == 0
+        return out[::-1].copy()
+
+
+def post_fxaa(ref: str) -> str:
+    """post.frag (FXAA main, post.frag:135-144) with the ES 3.00 header swap."""
+    with open(os.path.join(ref, "post.frag")) as f:
+        s = f.read()
+    s = re.sub(r"^\s*#version.*$", "", s, flags=re.M)
+    s = must_sub("gl_TexCoord[0]", "vec4(v_uv, 0.0, 0.0)", s)
+    s = must_sub("gl_FragColor = color;", "o_col = color;", s)
+    return ("#version 300 es\nprecision highp float;\nprecision highp int;\nprecision highp sampler2D;\n"
+            "in vec2 v_uv;\nout vec4 o_col;\n" + s)
+
+
+def unorm8(rgba):
+    q = np.clip(np.rint(np.clip(np.nan_to_num(rgba, nan=0.0), 0.0, 1.0) * 255.0), 0, 255).astype(np.uint32)
+    return q[..., 0] | (q[..., 1] << 8) | (q[..., 2] << 16) | (q[..., 3] << 24)
+
+
+def fxaa_inputs():
+    """(name, H x W RGBA8) inputs: two ray-march goldens and a synthetic edge pattern."""
+    out = []
+    for nm in ("T_64_P0", "O_96x54_P2"):
+        z = np.load(os.path.join(HERE, nm + ".npz"), allow_pickle=False)
+        out.append(("FXAA_" + nm, unorm8(z["rgba"])))
+    rng = np.random.default_rng(20261015)
+    H, W = 37, 61
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = np.zeros((H, W, 4), np.float32)
+    img[..., 3] = 1.0
+    img[..., 0] = (xx * 0.7 + yy * 1.3 > 30).astype(np.float32)          # a slanted edge
+    img[..., 1] = ((xx // 5 + yy // 4) % 2).astype(np.float32) * 0.8     # blocks
+    img[..., 2] = rng.uniform(0, 1, (H, W)).astype(np.float32)           # noise
+    out.append(("FXAA_synthetic_61x37", unorm8(img)))
+    return out
+
+
 # ------------------------------------------------------------- fixtures
 
 FIXTURES = [
@@ -378,6 +448,17 @@ def main():
                             meta=json.dumps(meta))
         print(f"{name}: {dt:.2f}s mean={rgba[..., :3].mean():.4f} evals/px={cnt[..., 0].mean():.2f} "
               f"nan={int(np.isnan(rgba).sum())}")
+    # the FXAA post pass (post.frag), next to the hot path
+    for name, img in fxaa_inputs():
+        if args.only and args.only not in name:
+            continue
+        H, W = img.shape
+        g = GL(W, H)
+        out = g.post(g.program(post_fxaa(args.ref)), img, (W, H))
+        meta = dict(pass_="post.frag fxaa", W=W, H=H, sampler="NEAREST, CLAMP_TO_EDGE", renderer=g.renderer,
+                    generator="tests/golden/make_goldens.py")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), input=img, output=out, meta=json.dumps(meta))
+        print(f"{name}: changed pixels {float(np.mean(out != img[::-1])):.3f}")
 
 
 if __name__ == "__main__":
