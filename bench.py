@@ -18,7 +18,7 @@ runs are uninstrumented.
 
 Usage: python bench.py [--gpus N --steps K --warmup W] [--scene T|O|S0]
        [--size 4096] [--max-steps 256] [--pose P0] [--band 16]
-       [--fmt rgba8|float4] [--kernel auto|direct|wave] [--cpu-seconds 12]
+       [--fmt rgba8|float4] [--kernel auto|tile16|tile8] [--cpu-seconds 12]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
 from __future__ import annotations
@@ -48,9 +48,9 @@ def parse():
     ap.add_argument("--pose", default="P0")
     ap.add_argument("--band", type=int, default=16)
     ap.add_argument("--chunks", type=int, default=None,
-                    help="pipeline chunks per frame for N > 1 (render k+1 while gathering k); default 1 at N=1, 4 else")
+                    help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
-    ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "wave"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "tile16", "tile8"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
@@ -151,7 +151,7 @@ def main():
     r.set_params(max_steps=args.max_steps, shadow_max_steps=0, kernel=args.kernel)
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream)
-    chunks = args.chunks if args.chunks is not None else (1 if world == 1 else 4)
+    chunks = args.chunks if args.chunks is not None else 1
     fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks)
 
     # instrumented run: ray-steps of this rank's rows, summed over ranks
@@ -166,7 +166,8 @@ def main():
     evals_rank, evals_frame = int(ev_rank.item()), int(ev_total.item())
 
     for _ in range(args.warmup):
-        fr.render()
+        fr.submit()
+    fr.flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -177,7 +178,8 @@ def main():
            for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        fr.render(events=evs[i])
+        fr.submit(events=evs[i])  # frame i's gather overlaps frame i+1's render
+    fr.flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -49,7 +49,7 @@ typedef struct rm_params {
     int32_t max_steps;        /* MAX_MARCHING_STEPS, common.frag:15 (default 128)        */
     int32_t shadow_max_steps; /* softshadow2 cap; 0 = unbounded as common.frag:814       */
     int32_t count_evals;      /* 1: instrumented kernel, rm_stats.evals = sceneSDF calls */
-    int32_t kernel;           /* 0 = auto, 1 = direct (lane per pixel), 2 = wave state machine */
+    int32_t kernel;           /* workgroup tiling: 0 auto (= 2), 1 16x16 px (4 waves), 2 8x8 px (1 wave), 3 16x4 px (1 wave) */
 } rm_params;
 
 typedef struct rm_stats {

@@ -170,10 +170,11 @@ rm_status ensure_staging(rm_ctx *ctx, size_t bytes) {
     return RM_OK;
 }
 
+// rm_params.kernel: 0 auto, 1 = 16x16-pixel workgroups, 2 = 8x8-pixel workgroups
 int pick_kernel(const rm_ctx *c) {
-    if (c->params.kernel == 1) return rm::KERNEL_DIRECT;
-    if (c->params.kernel == 2) return rm::KERNEL_WAVE;
-    return rm::has_wave_kernel_host(c->scene) ? rm::KERNEL_WAVE : rm::KERNEL_DIRECT;
+    if (c->params.kernel == 1) return rm::KERNEL_TILE16;
+    if (c->params.kernel == 3) return rm::KERNEL_TILE16X4;
+    return rm::KERNEL_TILE8;  // 0 auto, 2: measured fastest on every config
 }
 
 // the pass over packed rows [row0, row0 + count) of a shard: device output,
@@ -325,7 +326,7 @@ rm_status rm_set_uniform3f(rm_ctx *ctx, const char *name, float x, float y, floa
 
 rm_status rm_set_params(rm_ctx *ctx, const rm_params *p) {
     if (!ctx || !p) return RM_ERR_INVALID_ARGUMENT;
-    if (p->max_steps < 0 || p->max_steps > (1 << 20) || p->shadow_max_steps < 0 || p->kernel < 0 || p->kernel > 2)
+    if (p->max_steps < 0 || p->max_steps > (1 << 20) || p->shadow_max_steps < 0 || p->kernel < 0 || p->kernel > 3)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_set_params: out of range");
     ctx->params = *p;
     return RM_OK;

@@ -198,12 +198,22 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p) {
     } else if constexpr (SC == SCENE_T) {
         return menger<EXACT>(sponge_space<EXACT>(F, p));  // template.frag:41 (repaired)
     } else {  // output_shader.frag:38-48
-        float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
-        float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
         float d3 = p.y;
-        float m;
-        float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
-        float t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
+        float m, t2;
+        // Lower bounds of the sphere and the cube (Chebyshev <= Euclidean
+        // distance, exactly also after rounding), and sminCubic lowers the min
+        // by at most k/6: if even the bound of t1 is past the floor by more than
+        // the blend width, t2 = sminCubic(t1, plane) is exactly the plane.
+        float lb1 = fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))) - 1.0f;
+        float lb2 = fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f))) - 1.0f;
+        if (fminf(lb1, lb2) - 0.0834f >= d3 + 0.51f) {
+            t2 = d3;
+        } else {
+            float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
+            float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+            float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
+            t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
+        }
         // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width
         // k = 0.33 (with a margin far above rounding), sminCubic's h is 0 and the
         // result is exactly t2: the sponge's folds are not needed.

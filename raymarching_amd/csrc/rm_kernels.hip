@@ -11,7 +11,6 @@
 
 #include "rm_device.h"
 #include "rm_launch.h"
-#include "rm_render_wave.h"
 
 namespace rm {
 
@@ -61,8 +60,6 @@ hipError_t launch_render(int scene, const FrameConst& F, float4* out, unsigned l
     default: return hipErrorInvalidValue;
     }
 }
-
-bool has_wave_kernel_host(int scene) { return has_wave_kernel(scene); }
 
 template <typename E>
 static hipError_t deinterleave_t(const E* gathered, E* out, int W, int H, int band, int nshards, int rows_per_shard,

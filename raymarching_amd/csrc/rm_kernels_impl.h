@@ -7,7 +7,6 @@
 #include "rm_device.h"
 #include "rm_launch.h"
 #include "rm_render_direct.h"
-#include "rm_render_wave.h"
 
 namespace rm {
 
@@ -24,12 +23,22 @@ __device__ __forceinline__ V3 render_pixel(const FrameConst& F, V3 ro, V3 rd, ui
     else return render_O<SC>(F, ro, rd, cnt);
 }
 
-template <int SC, bool COUNT>
-__global__ __launch_bounds__(256) void rm_render_direct(FrameConst F, float4* __restrict__ out,
-                                                          unsigned long long* __restrict__ evals) {
+// Workgroup shapes (KernelKind): KERNEL_TILE16 = 16x16 pixels as 2x2 waves
+// of 8x8; KERNEL_TILE8 = one 8x8-pixel wave per workgroup (the dispatcher
+// then refills CUs at wave granularity, which shortens the tail of small or
+// uneven launches); KERNEL_TILE16X4 = one 16x4-pixel wave.
+template <int K> struct Tiling;
+template <> struct Tiling<KERNEL_TILE16> { static constexpr int TW = 16, TH = 16, WPB = 4, LW = 8; };
+template <> struct Tiling<KERNEL_TILE8> { static constexpr int TW = 8, TH = 8, WPB = 1, LW = 8; };
+template <> struct Tiling<KERNEL_TILE16X4> { static constexpr int TW = 16, TH = 4, WPB = 1, LW = 16; };
+
+template <int SC, bool COUNT, int K>
+__global__ __launch_bounds__(64 * Tiling<K>::WPB) void rm_render_direct(FrameConst F, float4* __restrict__ out,
+                                                                        unsigned long long* __restrict__ evals) {
+    using T = Tiling<K>;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
-    const int j = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
+    const int x = blockIdx.x * T::TW + (w & 1) * 8 + (lane % T::LW);
+    const int j = blockIdx.y * T::TH + (w >> 1) * 8 + (lane / T::LW);
     uint32_t cnt = 0;
     if (x < F.W && j < F.nrows) {
         const int y = shard_row(F, F.row0 + j);
@@ -46,14 +55,20 @@ __global__ __launch_bounds__(256) void rm_render_direct(FrameConst F, float4* __
     }
 }
 
-template <int SC>
-hipError_t launch_scene(const FrameConst& F, float4* out, unsigned long long* evals, int kernel,
-                               hipStream_t s) {
-    if (kernel == KERNEL_WAVE && has_wave_kernel(SC)) return launch_wave<SC>(F, out, evals, s);
-    dim3 grid((F.W + 15) / 16, (F.nrows + 15) / 16), block(256);
-    if (evals) hipLaunchKernelGGL((rm_render_direct<SC, true>), grid, block, 0, s, F, out, evals);
-    else hipLaunchKernelGGL((rm_render_direct<SC, false>), grid, block, 0, s, F, out, evals);
+template <int SC, int K>
+hipError_t launch_direct(const FrameConst& F, float4* out, unsigned long long* evals, hipStream_t s) {
+    using T = Tiling<K>;
+    dim3 grid((F.W + T::TW - 1) / T::TW, (F.nrows + T::TH - 1) / T::TH), block(64 * T::WPB);
+    if (evals) hipLaunchKernelGGL((rm_render_direct<SC, true, K>), grid, block, 0, s, F, out, evals);
+    else hipLaunchKernelGGL((rm_render_direct<SC, false, K>), grid, block, 0, s, F, out, evals);
     return hipGetLastError();
+}
+
+template <int SC>
+hipError_t launch_scene(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
+    if (kernel == KERNEL_TILE16) return launch_direct<SC, KERNEL_TILE16>(F, out, evals, s);
+    if (kernel == KERNEL_TILE16X4) return launch_direct<SC, KERNEL_TILE16X4>(F, out, evals, s);
+    return launch_direct<SC, KERNEL_TILE8>(F, out, evals, s);
 }
 
 }  // namespace rm

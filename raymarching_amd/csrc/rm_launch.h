@@ -8,7 +8,7 @@
 
 namespace rm {
 
-enum KernelKind : int { KERNEL_DIRECT = 0, KERNEL_WAVE = 1 };
+enum KernelKind : int { KERNEL_TILE16 = 0, KERNEL_TILE8 = 1, KERNEL_TILE16X4 = 2 };
 
 hipError_t launch_render(int scene, const FrameConst& F, float4* out, unsigned long long* evals, int kernel,
                          hipStream_t s);
@@ -17,7 +17,6 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, int W, int H
 hipError_t launch_deinterleave_u32(const uint32_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
                                    int rows_per_shard, hipStream_t s);
 hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStream_t s);
-bool has_wave_kernel_host(int scene);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 
 }  // namespace rm

@@ -87,10 +87,14 @@ class DistributedFrame:
     stream.  ``fmt`` is "rgba8" (the displayed RenderTexture format, 4 B/px on
     the wire) or "float4" (full gl_FragColor, 16 B/px, used by parity tests).
 
-    ``chunks`` > 1 pipelines a frame: the packed rows are cut into that many
-    row ranges (the same cuts on every rank, so gathers line up); chunk k+1 is
-    rendered on the compute stream while chunk k's gather (async, on RCCL's
-    stream) moves over xGMI, leaving only the last chunk's transfer exposed.
+    Overlap of the gather (RCCL, xGMI) with rendering, two ways:
+    * ``submit()`` / ``flush()`` pipeline consecutive frames: frame k's gather
+      runs on RCCL's stream while frame k+1 renders (the wire buffers are
+      double-buffered); rank 0 de-interleaves frame k after frame k+1's render
+      was enqueued.  One render launch per frame per rank.
+    * ``chunks`` > 1 pipelines within a frame: the packed rows are cut into
+      that many ranges (same cuts on every rank) and chunk k+1 renders while
+      chunk k is gathered; it costs a launch tail per chunk.
     """
 
     def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None, chunks=1):
@@ -105,9 +109,13 @@ class DistributedFrame:
         chunks = max(1, min(int(chunks), rps))
         self.cuts = [round(c * rps / chunks) for c in range(chunks + 1)]
         self.local = torch.empty((rps, W, 4), dtype=torch.float32, device=dev)
-        self.local8 = torch.empty((rps, W), dtype=torch.int32, device=dev) if fmt == "rgba8" else None
-        wire = self.local8 if fmt == "rgba8" else self.local
-        self.gathered = (torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev)
+        nbuf = 2 if world > 1 else 1
+        if fmt == "rgba8":
+            self.wires = [torch.empty((rps, W), dtype=torch.int32, device=dev) for _ in range(nbuf)]
+        else:  # float4 renders straight into the slot being gathered
+            self.wires = [self.local] + [torch.empty_like(self.local) for _ in range(nbuf - 1)]
+        wire = self.wires[0]
+        self.gathered = ([torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev) for _ in range(2)]
                          if rank == 0 and world > 1 else None)
         if world == 1:
             self.frame = wire
@@ -116,44 +124,82 @@ class DistributedFrame:
             self.frame = torch.empty(shape, dtype=wire.dtype, device=dev)
         else:
             self.frame = None
+        self.k = 0            # frames submitted
+        self.pending = None   # (slot, [works]) of the frame whose gather is in flight
 
-    def _render_chunk(self, c, events=None):
+    @property
+    def local8(self):
+        return self.wires[0] if self.fmt == "rgba8" else None
+
+    def _pipelined(self):
+        import torch.distributed as dist
+        return self.world > 1 and dist.get_backend(self.group) != "gloo"
+
+    def _render_rows(self, j0, j1, slot, events=None):
         p = self.plan
-        j0, j1 = self.cuts[c], min(self.cuts[c + 1], self.nmine)
+        j1 = min(j1, self.nmine)
         if j1 <= j0:
             return
+        dst = self.local if self.fmt == "rgba8" else self.wires[slot]
         if events is not None:
             events[0].record()
-        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, self.local[j0:j1])
+        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, dst[j0:j1])
         if events is not None:
             events[1].record()
         if self.fmt == "rgba8":
-            self.r.pack_rgba8(self.local[j0:j1], out=self.local8[j0:j1])
+            self.r.pack_rgba8(self.local[j0:j1], out=self.wires[slot][j0:j1])
+
+    def _gather_async(self, slot, j0, j1):
+        import torch.distributed as dist
+        g = self.gathered[slot] if self.rank == 0 else None
+        glist = [g[r, j0:j1] for r in range(self.world)] if self.rank == 0 else None
+        return dist.gather(self.wires[slot][j0:j1], gather_list=glist, dst=0, group=self.group, async_op=True)
+
+    def _deinterleave(self, slot):
+        p = self.plan
+        self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered[slot], out=self.frame)
 
     def render_local(self, stats=False):
         """This rank's rows only (no gather); stats: one synchronous launch."""
         p = self.plan
         return self.r.render_band(p.W, p.H, p.band, p.nshards, self.rank, out=self.local[: self.nmine], stats=stats)
 
-    def render(self, events=None):
-        """One frame.  events: optional list of (start, end) torch.cuda.Event
-        pairs, one per chunk, recorded around the render kernels."""
-        import torch.distributed as dist
-
-        p = self.plan
-        wire = self.local8 if self.fmt == "rgba8" else self.local
-        pipelined = self.world > 1 and dist.get_backend(self.group) != "gloo"
+    def submit(self, events=None):
+        """Enqueue one frame.  With N > 1 its gather stays in flight until the
+        next submit()/flush().  events: optional list of (start, end)
+        torch.cuda.Event pairs, one per chunk, recorded around the renders."""
+        slot = self.k % len(self.wires)
+        self.k += 1
+        nch = len(self.cuts) - 1
         works = []
-        for c in range(len(self.cuts) - 1):
-            self._render_chunk(c, None if events is None else events[c])
-            if pipelined:
-                j0, j1 = self.cuts[c], self.cuts[c + 1]
-                glist = [self.gathered[r, j0:j1] for r in range(self.world)] if self.rank == 0 else None
-                works.append(dist.gather(wire[j0:j1], gather_list=glist, dst=0, group=self.group, async_op=True))
-        if self.world > 1 and not pipelined:  # gloo: one host-staged gather
-            gather_to_root(wire, p, self.rank, group=self.group, out=self.gathered)
-        for w in works:
-            w.wait()
-        if self.world > 1 and self.rank == 0:
-            self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered, out=self.frame)
+        for c in range(nch):
+            self._render_rows(self.cuts[c], self.cuts[c + 1], slot, None if events is None else events[c])
+            if self._pipelined():
+                works.append(self._gather_async(slot, self.cuts[c], self.cuts[c + 1]))
+        if self.world > 1 and not self._pipelined():  # gloo: one host-staged gather, completed here
+            gather_to_root(self.wires[slot], self.plan, self.rank, group=self.group,
+                           out=self.gathered[slot] if self.rank == 0 else None)
+            works = None
+        prev, self.pending = self.pending, (slot, works) if self.world > 1 else None
+        if prev is not None:
+            self._complete(prev)
         return self.frame
+
+    def _complete(self, item):
+        slot, works = item
+        for w in works or ():
+            w.wait()
+        if self.rank == 0:
+            self._deinterleave(slot)
+
+    def flush(self):
+        """Finish the frame in flight (rank 0: its de-interleaved frame is in .frame)."""
+        if self.pending is not None:
+            item, self.pending = self.pending, None
+            self._complete(item)
+        return self.frame
+
+    def render(self, events=None):
+        """One complete frame (submit + flush)."""
+        self.submit(events)
+        return self.flush()
