@@ -148,8 +148,7 @@ __device__ __forceinline__ float menger(V3 p) {
 // transformR(p - vec3(0,3,0), vec3(180, 2t, 0)): row vector times rotationY
 // then rotationX (common.frag:434-441); rotation Z is the identity.
 template <bool EXACT>
-__device__ __forceinline__ V3 sponge_space(const FrameConst& F, V3 p) {
-    float x = p.x, y = p.y - 3.0f, z = p.z;
+__device__ __forceinline__ V3 sponge_rot(const FrameConst& F, float x, float y, float z) {
     if constexpr (EXACT) {
         float x1 = x * F.ry_c + z * F.ry_s;
         float z1 = x * -F.ry_s + z * F.ry_c;
@@ -163,6 +162,22 @@ __device__ __forceinline__ V3 sponge_space(const FrameConst& F, V3 p) {
         float z2 = fmaf(z1, F.rx_c, y * F.rx_s);
         return v3(x1, y2, z2);
     }
+}
+template <bool EXACT>
+__device__ __forceinline__ V3 sponge_space(const FrameConst& F, V3 p) {
+    return sponge_rot<EXACT>(F, p.x, p.y - 3.0f, p.z);
+}
+
+// A ray in sponge space: the transform is affine, so ro + rd t maps to
+// o + d t (scene T's marches step there; only roundings differ).
+struct LinRay {
+    V3 o, d;
+};
+__device__ __forceinline__ LinRay sponge_ray(const FrameConst& F, V3 ro, V3 rd) {
+    return LinRay{sponge_space<false>(F, ro), sponge_rot<false>(F, rd.x, rd.y, rd.z)};
+}
+__device__ __forceinline__ V3 at(const LinRay& r, float t) {
+    return v3(fmaf(r.d.x, t, r.o.x), fmaf(r.d.y, t, r.o.y), fmaf(r.d.z, t, r.o.z));
 }
 
 // sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4

@@ -124,6 +124,53 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
     return res;
 }
 
+// softShadow2 for scene T (fast math), stepping in sponge space and free of
+// divisions and square roots.  With P = 2 ph the reference's y = h^2/P gives
+//   k sqrt(h^2 - y^2) / (t - y) = k h sqrt(P^2 - h^2) / (t P - h^2),
+// and res is kept squared as num/den, candidates compared by cross-products.
+// Candidates with t - y <= 0 (k d / 0: inf or NaN) or h^2 < y^2 (sqrt NaN)
+// never lower res, as GLSL min(res, x) = x < res ? x : res.  On the first step
+// ph = 1e20 makes y vanish: the candidate is k h / t (Q = 1, D = t below).
+__device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
+                                                uint32_t& cnt) {
+    const float k2 = 16.0f;  // k = 4
+    float num = 1.0f, den = 1.0f, P = 0.0f;
+    bool first = true;
+    int it = 0;
+    for (float t = mint; t < maxt;) {
+        if (F.shadow_max_steps > 0 && it++ >= F.shadow_max_steps) break;
+        float h = menger<false>(at(s, t));
+        cnt++;
+        if (h < 0.001f) return 0.0f;
+        float h2 = h * h;
+        float Q = first ? 1.0f : fmaf(P, P, -h2);
+        float D = first ? t : fmaf(t, P, -h2);
+        float cn = k2 * h2 * Q, cd = D * D;
+        if (D > 0.0f && Q >= 0.0f && cn * den < num * cd) {
+            num = cn;
+            den = cd;
+        }
+        P = 2.0f * h;
+        first = false;
+        t = fmaf(h, 0.1f, t + 0.001f);
+    }
+    return __builtin_amdgcn_sqrtf(num * __builtin_amdgcn_rcpf(den));
+}
+
+// castRay (common.frag:931-954) for scene T in sponge space; returns the
+// depth of the point the reference returns (ZFAR on escape)
+__device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s, uint32_t& cnt) {
+    float depth = ZNEAR;
+    for (int i = 0; i < F.max_steps; i++) {
+        float dist = menger<false>(at(s, depth));
+        cnt++;
+        if (dist < 0.001f) return depth;
+        depth += dist;
+        if (depth >= ZFAR) return ZFAR;
+    }
+    return depth;
+}
+
 // common.frag:850-866
 template <int SC>
 __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, uint32_t& cnt) {
@@ -279,18 +326,19 @@ __device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
 // template.frag:45-76 (scene T)
 __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
     constexpr int SC = SCENE_T;
-    V3 p = cast_ray<SC>(F, ro, rd, cnt);
+    V3 p = ro + rd * cast_ray_T(F, sponge_ray(F, ro, rd), cnt);
     V3 n = normal_fast<SC>(F, p, cnt);
     // getColorReflect (common.frag:991-1002); its dead nr normal is skipped
     V3 rdir = reflect(rd, n);
-    V3 pr = cast_ray<SC>(F, p + rdir * 0.01f, rdir, cnt);
+    V3 ror = p + rdir * 0.01f;
+    V3 pr = ror + rdir * cast_ray_T(F, sponge_ray(F, ror, rdir), cnt);
     float c = clamp01(length(pr - p) * (1.0f / 3.0f));
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     float ld2 = dot(Ld, Ld);
     V3 lightDir = Ld * __builtin_amdgcn_rsqf(ld2);
     float occ = ao_real<SC>(F, p, n, cnt);
-    float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
+    float sha = soft_shadow2_T(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     float fre = clamp01(1.0f + dot(n, rd));
