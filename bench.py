@@ -196,15 +196,35 @@ def main():
 
     if rank == 0:
         F = rm.FLOP_PER_EVAL[args.scene]
-        ach = evals_rank * F / (kern / 1e3) / 1e12
+        flop_rank = st["flop"]
+        ach = flop_rank / (kern / 1e3) / 1e12
         out_bytes = W * fr.plan.count(0) * 16
-        traffic = None
+        pmc = {}
         try:
             pm = json.load(open(args.pmc))
             key = f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}" + ("" if world == 1 else f"_n{world}")
-            traffic = pm.get(key, {}).get("hbm_bytes_per_launch")
+            pmc = pm.get(key, {})
         except (OSError, ValueError):
             pass
+        roof = {
+            "bound": "valu", "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / PEAK_FP32_TFLOPS, "traffic": pmc.get("hbm_bytes_per_launch"),
+            "algorithmic_flop_per_launch": flop_rank, "ray_steps_per_launch": evals_rank,
+            "flop_per_ray_step": flop_rank / max(1, evals_rank),
+            "flop_note": "SURVEY.md 8(d) per-term tally over the terms each ray-step evaluates; Menger folds "
+                         "(and scene O's primitives) that an exact early exit skips are not counted",
+            "reference_tally_flop_per_ray_step": F,
+            "reference_equivalent_tflops": evals_rank * F / (kern / 1e3) / 1e12,
+            "hbm": {"achieved": out_bytes / (kern / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": out_bytes / (kern / 1e3) / 1e9 / PEAK_HBM_GBS,
+                    "algorithmic_bytes_per_launch": out_bytes},
+        }
+        if "SQ_INSTS_VALU" in pmc:
+            # executed vector instructions (PMC, per launch) against the issue peak: one wave64
+            # VALU instruction per 2 cycles per SIMD (MI355X_MICROARCH.md), 1024 SIMDs, 2.4 GHz
+            insts = pmc["SQ_INSTS_VALU"]
+            roof["valu_issue"] = {"insts_per_launch": insts, "frac": insts * 2 / (kern / 1e3 * 2.4e9 * 1024),
+                                  "source": pmc.get("source")}
         res = {
             "metric": "ray-steps/sec + frames/sec at 4096\u00d74096, 1/2/4/8 MI355X",
             "value": evals_frame * args.steps / elapsed,
@@ -228,14 +248,7 @@ def main():
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
             },
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max,
-            "roofline": {
-                "bound": "valu", "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic,
-                "flop_per_ray_step": F, "ray_steps_per_launch": evals_rank,
-                "hbm": {"achieved": out_bytes / (kern / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": out_bytes / (kern / 1e3) / 1e9 / PEAK_HBM_GBS,
-                        "algorithmic_bytes_per_launch": out_bytes},
-            },
+            "roofline": roof,
         }
         if fr.frame is not None and fr.fmt == "rgba8":
             res["post_pass"] = time_fxaa(r, fr.frame, stream)

@@ -57,6 +57,9 @@ typedef struct rm_stats {
     uint64_t pixels; /* pixels rendered                                                */
     float kernel_ms; /* device time of the render kernel (HIP events on the ctx stream) */
     int32_t scene;   /* scene id that ran                                              */
+    uint64_t flop;   /* algorithmic FLOP of those calls, when count_evals: the per-term
+                        tally of SURVEY.md 8(d) over the terms evaluated (exact early
+                        exits skip Menger folds and scene O's primitives)          */
 } rm_stats;
 
 /* Create a context on HIP device `device`.  Scene unset, params default. */
@@ -126,8 +129,16 @@ rm_status rm_deinterleave_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards
 /* float RGBA -> RGBA8 unorm (round to nearest, clamped), device pointers. */
 rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t *out);
 
-/* rm_render + rm_pack_rgba8 into a W*H uint32 target (device or host). */
+/* rm_render into a W*H RGBA8 target (device or host): the kernel packs each
+ * pixel as rm_pack_rgba8 does (bit-identical to rm_render + rm_pack_rgba8),
+ * writing 4 B/px instead of 16. */
 rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats);
+
+/* rm_render_band / rm_render_rows into RGBA8 rows (W uint32 per row). */
+rm_status rm_render_band_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, uint32_t *out,
+                               rm_stats *stats);
+rm_status rm_render_rows_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin,
+                               int row_count, uint32_t *out, rm_stats *stats);
 
 /* The reference's FXAA post pass (post.frag:16-61, :135-144) over an RGBA8
  * frame: in/out W*H RGBA8 words (device, distinct), sampled as the reference's

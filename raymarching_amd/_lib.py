@@ -19,8 +19,9 @@ STATUS = {0: "RM_OK", 1: "RM_ERR_INVALID_ARGUMENT", 2: "RM_ERR_FILE", 3: "RM_ERR
 # every symbol include/rm.h declares
 EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_set_uniform2f",
            "rm_set_uniform3f", "rm_set_params", "rm_get_params", "rm_set_stream", "rm_synchronize",
-           "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8", "rm_pack_rgba8",
-           "rm_render_rgba8", "rm_fxaa", "rm_last_error", "rm_status_string")
+           "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8",
+           "rm_pack_rgba8",
+           "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_last_error", "rm_status_string")
 
 
 class RmParams(ctypes.Structure):
@@ -30,11 +31,11 @@ class RmParams(ctypes.Structure):
 
 class RmStats(ctypes.Structure):
     _fields_ = [("evals", ctypes.c_uint64), ("pixels", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
-                ("scene", ctypes.c_int32)]
+                ("scene", ctypes.c_int32), ("flop", ctypes.c_uint64)]
 
     def as_dict(self):
         return dict(evals=int(self.evals), pixels=int(self.pixels), kernel_ms=float(self.kernel_ms),
-                    scene=int(self.scene))
+                    scene=int(self.scene), flop=int(self.flop))
 
 
 class RmError(RuntimeError):
@@ -83,6 +84,10 @@ def lib() -> ctypes.CDLL:
         "rm_deinterleave_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_pack_rgba8": ([vp, c.c_int64, vp, vp], c.c_int),
         "rm_render_rgba8": ([vp, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
+        "rm_render_band_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)],
+                                 c.c_int),
+        "rm_render_rows_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp,
+                                  c.POINTER(RmStats)], c.c_int),
         "rm_fxaa": ([vp, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_last_error": ([vp], cp),
         "rm_status_string": ([c.c_int], cp),

@@ -129,11 +129,27 @@ class Renderer:
         return (out, s.as_dict()) if stats else out
 
     def render_rows(self, W, H, band, nshards, shard, row_begin, row_count, out, stats=False):
-        """Packed rows [row_begin, row_begin + row_count) of a shard into `out`."""
-        _check_out(out, row_count * W * 4)
+        """Packed rows [row_begin, row_begin + row_count) of a shard into `out`
+        (float32 [rows, W, 4], or int32 [rows, W] RGBA8 words: the kernel packs)."""
+        torch = _torch()
+        rgba8 = out.dtype != torch.float32
+        _check_out(out, row_count * W * (1 if rgba8 else 4))
         s = RmStats()
-        check(lib().rm_render_rows(self._ctx, int(W), int(H), int(band), int(nshards), int(shard), int(row_begin),
-                                   int(row_count), self._ptr(out), ctypes.byref(s) if stats else None), self._ctx)
+        fn = lib().rm_render_rows_rgba8 if rgba8 else lib().rm_render_rows
+        check(fn(self._ctx, int(W), int(H), int(band), int(nshards), int(shard), int(row_begin), int(row_count),
+                 self._ptr(out), ctypes.byref(s) if stats else None), self._ctx)
+        return (out, s.as_dict()) if stats else out
+
+    def render_band_rgba8(self, W, H, band, nshards, shard, out=None, stats=False):
+        """render_band into RGBA8 words ([rows, W] int32)."""
+        torch = _torch()
+        n = shard_rows(H, band, nshards, shard)
+        if out is None:
+            out = torch.empty((n, W), dtype=torch.int32, device=f"cuda:{self.device}")
+        _check_out(out, n * W)
+        s = RmStats()
+        check(lib().rm_render_band_rgba8(self._ctx, int(W), int(H), int(band), int(nshards), int(shard),
+                                         self._ptr(out), ctypes.byref(s) if stats else None), self._ctx)
         return (out, s.as_dict()) if stats else out
 
     def deinterleave(self, W, H, band, nshards, rows_per_shard, gathered, out=None):
@@ -173,6 +189,8 @@ class Renderer:
         torch = _torch()
         if out is None:
             out = torch.empty((H, W), dtype=torch.int32, device=f"cuda:{self.device}")
+        if hasattr(out, "is_cuda"):
+            _check_out(out, H * W)
         s = RmStats()
         check(lib().rm_render_rgba8(self._ctx, W, H, self._ptr(out), ctypes.byref(s) if stats else None),
               self._ctx)

@@ -179,23 +179,24 @@ int pick_kernel(const rm_ctx *c) {
 
 // the pass over packed rows [row0, row0 + count) of a shard: device output,
 // optional stats (synchronous when given)
-rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, float4 *out,
-                     rm_stats *stats) {
+rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, void *out,
+                     bool rgba8, rm_stats *stats) {
     FrameConst F = frame_const(ctx, W, H, band, nshards, shard, count);
     F.row0 = row0;
     bool cnt = ctx->params.count_evals != 0;
-    if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, sizeof(unsigned long long), ctx->stream));
+    if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 2 * sizeof(unsigned long long), ctx->stream));
     if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-    hipError_t e = rm::launch_render(ctx->scene, F, out, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
+    hipError_t e = rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) {
         RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         RM_HIP(hipEventSynchronize(ctx->ev1));
         float ms = 0.0f;
         RM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-        unsigned long long ev = 0;
-        if (cnt) RM_HIP(hipMemcpy(&ev, ctx->d_evals, sizeof(ev), hipMemcpyDeviceToHost));
-        stats->evals = ev;
+        unsigned long long ev[2] = {0, 0};
+        if (cnt) RM_HIP(hipMemcpy(ev, ctx->d_evals, sizeof(ev), hipMemcpyDeviceToHost));
+        stats->evals = ev[0];
+        stats->flop = ev[1];
         stats->pixels = (uint64_t)W * (uint64_t)count;
         stats->kernel_ms = ms;
         stats->scene = ctx->scene;
@@ -203,9 +204,9 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     return RM_OK;
 }
 
-// row_count < 0: every packed row from row_begin on
+// row_count < 0: every packed row from row_begin on; out: float4 or RGBA8 rows
 rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
-                     float *out, rm_stats *stats) {
+                     void *out, bool rgba8, rm_stats *stats) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
@@ -216,17 +217,16 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     if (row_begin < 0 || row_count < 0 || row_begin + row_count > n)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: packed row range outside the shard");
     if (row_count == 0) {  // e.g. more shards than bands: nothing to do
-        if (stats) *stats = rm_stats{0, 0, 0.0f, ctx->scene};
+        if (stats) *stats = rm_stats{0, 0, 0.0f, ctx->scene, 0};
         return RM_OK;
     }
     if (!out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: null output");
     RM_HIP(hipSetDevice(ctx->device));
-    if (is_device_ptr(out))
-        return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, reinterpret_cast<float4 *>(out), stats);
-    size_t bytes = (size_t)W * row_count * sizeof(float4);
+    if (is_device_ptr(out)) return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, out, rgba8, stats);
+    size_t bytes = (size_t)W * row_count * (rgba8 ? sizeof(uint32_t) : sizeof(float4));
     rm_status s = ensure_staging(ctx, bytes);
     if (s != RM_OK) return s;
-    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, ctx->staging, stats);
+    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, ctx->staging, rgba8, stats);
     if (s != RM_OK) return s;
     RM_HIP(hipMemcpyAsync(out, ctx->staging, bytes, hipMemcpyDeviceToHost, ctx->stream));
     RM_HIP(hipStreamSynchronize(ctx->stream));
@@ -248,7 +248,7 @@ rm_status rm_create(rm_ctx **out, int device) {
     rm_ctx *ctx = new rm_ctx();
     ctx->device = device;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_evals, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_evals, 2 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
     if (e != hipSuccess) {
@@ -351,17 +351,32 @@ rm_status rm_synchronize(rm_ctx *ctx) {
 }
 
 rm_status rm_render(rm_ctx *ctx, int W, int H, float *out, rm_stats *stats) {
-    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, out, stats);
+    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, out, false, stats);
 }
 
 rm_status rm_render_band(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out, rm_stats *stats) {
-    return render_any(ctx, W, H, band, nshards, shard, 0, -1, out, stats);
+    return render_any(ctx, W, H, band, nshards, shard, 0, -1, out, false, stats);
 }
 
 rm_status rm_render_rows(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
                          float *out, rm_stats *stats) {
     if (row_count < 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rows: negative row_count");
-    return render_any(ctx, W, H, band, nshards, shard, row_begin, row_count, out, stats);
+    return render_any(ctx, W, H, band, nshards, shard, row_begin, row_count, out, false, stats);
+}
+
+rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats) {
+    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, out, true, stats);
+}
+
+rm_status rm_render_band_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, uint32_t *out,
+                               rm_stats *stats) {
+    return render_any(ctx, W, H, band, nshards, shard, 0, -1, out, true, stats);
+}
+
+rm_status rm_render_rows_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin,
+                               int row_count, uint32_t *out, rm_stats *stats) {
+    if (row_count < 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rows_rgba8: negative row_count");
+    return render_any(ctx, W, H, band, nshards, shard, row_begin, row_count, out, true, stats);
 }
 
 rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows) {
@@ -420,30 +435,6 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) 
     RM_HIP(hipSetDevice(ctx->device));
     hipError_t e = rm::launch_fxaa(in, out, W, H, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "fxaa launch");
-    return RM_OK;
-}
-
-rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats) {
-    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
-    if (!out || W <= 0 || H <= 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rgba8: bad arguments");
-    if ((long long)W * H > (1LL << 31)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: frame too large");
-    if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
-    RM_HIP(hipSetDevice(ctx->device));
-    size_t npx = (size_t)W * H;
-    size_t fbytes = npx * sizeof(float4), bbytes = npx * sizeof(uint32_t);
-    // staging holds the float frame, followed by the packed frame when `out` is host memory
-    bool dev_out = is_device_ptr(out);
-    rm_status s = ensure_staging(ctx, fbytes + (dev_out ? 0 : bbytes));
-    if (s != RM_OK) return s;
-    s = render_dev(ctx, W, H, H, 1, 0, 0, H, ctx->staging, stats);
-    if (s != RM_OK) return s;
-    uint32_t *dst = dev_out ? out : reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(ctx->staging) + fbytes);
-    hipError_t e = rm::launch_pack_rgba8(ctx->staging, dst, npx, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "pack launch");
-    if (!dev_out) {
-        RM_HIP(hipMemcpyAsync(out, dst, bbytes, hipMemcpyDeviceToHost, ctx->stream));
-        RM_HIP(hipStreamSynchronize(ctx->stream));
-    }
     return RM_OK;
 }
 

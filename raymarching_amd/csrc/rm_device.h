@@ -84,6 +84,23 @@ __device__ __forceinline__ V3 refract(V3 I, V3 N, float eta) {
 
 // ------------------------------------------------------------------ SDFs
 
+// Work tally of the instrumented (COUNT) kernels: sceneSDF calls (ray-steps)
+// and the FLOP they needed, per term of SURVEY.md 8(d)'s tally (add, sub,
+// mul, min, max, cmp, floor = 1, FMA = 2, sqrt not counted).  Terms that an
+// exact early exit skips are not counted; the timed kernels never read it.
+struct Tally {
+    uint32_t evals = 0;
+    uint32_t flop = 0;
+};
+constexpr uint32_t FL_SPHERE = 9;      // sphere(): sub 3, dot 5, sub 1 (+ sqrt)
+constexpr uint32_t FL_TRANSFORM = 18;  // p - (0,3,0): 3; transformR's 3x3 rotation: 15
+constexpr uint32_t FL_LINRAY = 6;      // o + d t in sponge space: 3 FMA
+constexpr uint32_t FL_BOX = 17;        // sdBox(p, vec3(1))
+constexpr uint32_t FL_FOLD = 40;       // one mengersponge iteration (common.frag:663-676)
+constexpr uint32_t FL_CUBE = 21;       // cube()
+constexpr uint32_t FL_SMIN = 12;       // sminCubic, distance part
+constexpr uint32_t FL_BOUNDS = 16;     // scene O's two Chebyshev bounds and their test
+
 // x / b for a constant b, correctly rounded in all but rare cases: one
 // Markstein refinement of x * RN(1/b) (3 VALU ops; the reference's divisions
 // are GLSL "/" with <= 2.5 ulp).  Used on the parity-critical scene-O path.
@@ -104,22 +121,28 @@ __device__ __forceinline__ float div_const(float x, float b, float rb) {
 // (common.frag:595-600) is exactly mc: if mc <= 0 the length is 0 >= mc;
 // otherwise the rounded sum of squares is >= RN(mc*mc) and a correctly rounded
 // sqrt of RN(mc*mc) is mc, so the length is >= mc.  No sqrt.
+// max(|x| - 1, |y| - 1, |z| - 1) == max(|x|, |y|, |z|) - 1 exactly (rounding
+// is monotonic): one v_max3 with abs modifiers and one subtraction.
 __device__ __forceinline__ float sponge_box(V3 p) {
-    return fmaxf(fabsf(p.x) - 1.0f, fmaxf(fabsf(p.y) - 1.0f, fabsf(p.z) - 1.0f));
+    return fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z))) - 1.0f;
 }
-// the three folds, starting from the box term d; the result is >= d
+// The three folds, starting from the box term d; the result is >= d.
+// Fold m yields c = (med3(r) - 1)/s with med3(r) <= 2, so c <= 1/s: once
+// d >= 1/s the remaining folds cannot raise d (the `if (c > d)` of
+// common.frag:671 never fires) and the result is exactly d.  Lanes that are
+// not `active` never ask for a fold.  Far from the sponge (most march and
+// shadow steps) whole waves skip the folds.  (Wave-uniform variants of this
+// branch and of the march loops, __ballot-driven with lanes frozen by
+// selects, measured 1.13 ms against 0.93 ms per 4096^2 T frame: DESIGN.md.)
 template <bool EXACT>
-__device__ __forceinline__ float sponge_folds(V3 p, float d) {
+__device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool active = true) {
     constexpr float SH[3] = {0.5f, 1.5f, 4.5f};                      // s/2 before s *= 3
     constexpr float S3[3] = {3.0f, 9.0f, 27.0f};                     // s after s *= 3
     constexpr float INV[3] = {1.0f / 3.0f, 1.0f / 9.0f, 1.0f / 27.0f};
 #pragma unroll
     for (int m = 0; m < 3; m++) {
-        // Fold m yields c = (med3(r) - 1)/s with med3(r) <= 2, so c <= 1/s: once
-        // d >= 1/s the remaining folds cannot raise d (the `if (c > d)` of
-        // common.frag:671 never fires) and the result is exactly d.  Far from
-        // the sponge (most march and shadow steps) whole waves skip the folds.
-        if (d >= INV[m]) return d;
+        if (!(active && d < INV[m])) return d;
+        fl += FL_FOLD;
         float hx = p.x * SH[m], hy = p.y * SH[m], hz = p.z * SH[m];
         float ax = fmaf(2.0f, hx - floorf(hx), -1.0f);
         float ay = fmaf(2.0f, hy - floorf(hy), -1.0f);
@@ -136,13 +159,13 @@ __device__ __forceinline__ float sponge_folds(V3 p, float d) {
         }
         float med = __builtin_amdgcn_fmed3f(rx, ry, rz);
         float c = EXACT ? div_const(med - 1.0f, S3[m], INV[m]) : fmaf(med, INV[m], -INV[m]);
-        d = fmaxf(d, c);  // if (c > d) d = c;
+        d = c > d ? c : d;  // if (c > d) d = c;
     }
     return d;
 }
 template <bool EXACT>
-__device__ __forceinline__ float menger(V3 p) {
-    return sponge_folds<EXACT>(p, sponge_box(p));
+__device__ __forceinline__ float menger(V3 p, uint32_t& fl, bool active = true) {
+    return sponge_folds<EXACT>(p, sponge_box(p), fl, active);
 }
 
 // transformR(p - vec3(0,3,0), vec3(180, 2t, 0)): row vector times rotationY
@@ -179,6 +202,16 @@ __device__ __forceinline__ LinRay sponge_ray(const FrameConst& F, V3 ro, V3 rd) 
 __device__ __forceinline__ V3 at(const LinRay& r, float t) {
     return v3(fmaf(r.d.x, t, r.o.x), fmaf(r.d.y, t, r.o.y), fmaf(r.d.z, t, r.o.z));
 }
+// scene T's sceneSDF at depth t of a sponge-space ray: one ray-step on the
+// active lanes (inactive lanes compute a value nobody reads, without forcing
+// folds on the wave)
+__device__ __forceinline__ float menger_at(const LinRay& r, float t, Tally& n, bool active = true) {
+    if (active) {
+        n.evals++;
+        n.flop += FL_LINRAY + FL_BOX;
+    }
+    return menger<false>(at(r, t), n.flop, active);
+}
 
 // sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4
 template <bool EXACT>
@@ -207,11 +240,14 @@ __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
 // roundings (scene O's marches and normals, whose results feed the normal
 // hash); the fast form serves every other call.
 template <int SC, bool EXACT>
-__device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p) {
+__device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p, Tally& n) {
+    n.evals++;
     if constexpr (SC == SCENE_S0) {
+        n.flop += FL_SPHERE;
         return len3<EXACT>(p.x, p.y - 1.0f, p.z + 3.0f) - 1.0f;  // sphere(vec4(0,1,-3,1), p)
     } else if constexpr (SC == SCENE_T) {
-        return menger<EXACT>(sponge_space<EXACT>(F, p));  // template.frag:41 (repaired)
+        n.flop += FL_TRANSFORM + FL_BOX;
+        return menger<EXACT>(sponge_space<EXACT>(F, p), n.flop);  // template.frag:41 (repaired)
     } else {  // output_shader.frag:38-48
         float d3 = p.y;
         float m, t2;
@@ -221,9 +257,11 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p) {
         // the blend width, t2 = sminCubic(t1, plane) is exactly the plane.
         float lb1 = fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))) - 1.0f;
         float lb2 = fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f))) - 1.0f;
+        n.flop += FL_BOUNDS + FL_TRANSFORM + FL_BOX + 1;
         if (fminf(lb1, lb2) - 0.0834f >= d3 + 0.51f) {
             t2 = d3;
         } else {
+            n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
             float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
             float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
             float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
@@ -235,7 +273,8 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p) {
         V3 q = sponge_space<EXACT>(F, p);
         float mc = sponge_box(q);
         if (mc >= t2 + 0.34f) return t2;
-        float d0 = sponge_folds<EXACT>(q, mc);
+        float d0 = sponge_folds<EXACT>(q, mc, n.flop);
+        n.flop += FL_SMIN;
         return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
     }
 }
@@ -290,7 +329,8 @@ template <int SC>
 __device__ __forceinline__ Mat scene_mat(const FrameConst& F, V3 p) {
     if constexpr (SC == SCENE_O || SC == SCENE_OG) {
         constexpr bool glass = SC == SCENE_OG;
-        float d0 = menger<true>(sponge_space<true>(F, p));
+        uint32_t fl = 0;  // (the material evaluation is not a ray-step)
+        float d0 = menger<true>(sponge_space<true>(F, p), fl);
         float d1 = len3<true>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
         float d2 = cube<true>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
         float d3 = p.y;
@@ -340,6 +380,16 @@ __device__ __forceinline__ V3 apply_scattering(V3 color, V3 ro, V3 p) {
 }
 // output_shader.frag:178-182
 __device__ __forceinline__ V3 background(V3 ro, V3 rd) { return apply_scattering(v3s(0.0f), ro, ro + rd * ZFAR); }
+
+// RGBA8 unorm of the reference's RenderTexture: clamp, round to nearest
+// (NaN -> 0), R in the low byte
+__device__ __forceinline__ uint32_t to_unorm8(float c) {
+    c = fminf(fmaxf(c, 0.0f), 1.0f);  // NaN -> 0
+    return (uint32_t)__float2int_rn(c * 255.0f);
+}
+__device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float a) {
+    return to_unorm8(r) | (to_unorm8(g) << 8) | (to_unorm8(b) << 16) | (to_unorm8(a) << 24);
+}
 
 // ------------------------------------------------------------ hashing
 

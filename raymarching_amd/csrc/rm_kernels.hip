@@ -29,34 +29,31 @@ __global__ __launch_bounds__(256) void rm_deinterleave(const E* __restrict__ gat
     }
 }
 
-__device__ __forceinline__ uint32_t to_unorm8(float c) {
-    c = fminf(fmaxf(c, 0.0f), 1.0f);  // NaN -> 0
-    return (uint32_t)__float2int_rn(c * 255.0f);
-}
-
 __global__ __launch_bounds__(256) void rm_pack_rgba8(const float4* __restrict__ in, uint32_t* __restrict__ out,
                                                        size_t n) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         float4 v = in[i];
-        out[i] = to_unorm8(v.x) | (to_unorm8(v.y) << 8) | (to_unorm8(v.z) << 16) | (to_unorm8(v.w) << 24);
+        out[i] = pack_rgba8(v.x, v.y, v.z, v.w);
     }
 }
 
 // ------------------------------------------------------------- launchers
 
-hipError_t launch_scene_s0(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s);
-hipError_t launch_scene_t(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s);
-hipError_t launch_scene_o(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s);
-hipError_t launch_scene_og(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s);
+#define RM_SCENE_LAUNCHER(name) \
+    hipError_t name(const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel, hipStream_t s);
+RM_SCENE_LAUNCHER(launch_scene_s0)
+RM_SCENE_LAUNCHER(launch_scene_t)
+RM_SCENE_LAUNCHER(launch_scene_o)
+RM_SCENE_LAUNCHER(launch_scene_og)
 
-hipError_t launch_render(int scene, const FrameConst& F, float4* out, unsigned long long* evals, int kernel,
+hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
                          hipStream_t s) {
     if (F.W <= 0 || F.nrows <= 0) return hipSuccess;
     switch (scene) {
-    case SCENE_S0: return launch_scene_s0(F, out, evals, kernel, s);
-    case SCENE_T: return launch_scene_t(F, out, evals, kernel, s);
-    case SCENE_O: return launch_scene_o(F, out, evals, kernel, s);
-    case SCENE_OG: return launch_scene_og(F, out, evals, kernel, s);
+    case SCENE_S0: return launch_scene_s0(F, out, rgba8, evals, kernel, s);
+    case SCENE_T: return launch_scene_t(F, out, rgba8, evals, kernel, s);
+    case SCENE_O: return launch_scene_o(F, out, rgba8, evals, kernel, s);
+    case SCENE_OG: return launch_scene_og(F, out, rgba8, evals, kernel, s);
     default: return hipErrorInvalidValue;
     }
 }

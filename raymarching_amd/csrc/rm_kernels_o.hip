@@ -9,11 +9,13 @@
 
 namespace rm {
 
-hipError_t launch_scene_o(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
-    return launch_scene<SCENE_O>(F, out, evals, kernel, s);
+hipError_t launch_scene_o(const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
+                           hipStream_t s) {
+    return launch_scene<SCENE_O>(F, out, rgba8, evals, kernel, s);
 }
-hipError_t launch_scene_og(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
-    return launch_scene<SCENE_OG>(F, out, evals, kernel, s);
+hipError_t launch_scene_og(const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
+                           hipStream_t s) {
+    return launch_scene<SCENE_OG>(F, out, rgba8, evals, kernel, s);
 }
 
 }  // namespace rm

@@ -3,11 +3,13 @@
 
 namespace rm {
 
-hipError_t launch_scene_s0(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
-    return launch_scene<SCENE_S0>(F, out, evals, kernel, s);
+hipError_t launch_scene_s0(const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
+                           hipStream_t s) {
+    return launch_scene<SCENE_S0>(F, out, rgba8, evals, kernel, s);
 }
-hipError_t launch_scene_t(const FrameConst& F, float4* out, unsigned long long* evals, int kernel, hipStream_t s) {
-    return launch_scene<SCENE_T>(F, out, evals, kernel, s);
+hipError_t launch_scene_t(const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
+                           hipStream_t s) {
+    return launch_scene<SCENE_T>(F, out, rgba8, evals, kernel, s);
 }
 
 }  // namespace rm

@@ -10,7 +10,8 @@ namespace rm {
 
 enum KernelKind : int { KERNEL_TILE16 = 0, KERNEL_TILE8 = 1, KERNEL_TILE16X4 = 2 };
 
-hipError_t launch_render(int scene, const FrameConst& F, float4* out, unsigned long long* evals, int kernel,
+// out: W-wide rows of float4 (rgba8 = false) or RGBA8 words (rgba8 = true)
+hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
                          hipStream_t s);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, int W, int H, int band, int nshards,
                                int rows_per_shard, hipStream_t s);

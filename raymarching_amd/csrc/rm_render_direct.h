@@ -35,12 +35,12 @@ __device__ __forceinline__ float mpow(float x, float y) {
 // the scene distance for marches and normals (exact for scene O), and for
 // the AO / shadow / thickness probes, whose results are smooth in the distance
 template <int SC>
-__device__ __forceinline__ float dist_march(const FrameConst& F, V3 p) {
-    return scene_dist<SC, !FastMath<SC>::value>(F, p);
+__device__ __forceinline__ float dist_march(const FrameConst& F, V3 p, Tally& cnt) {
+    return scene_dist<SC, !FastMath<SC>::value>(F, p, cnt);
 }
 template <int SC>
-__device__ __forceinline__ float dist_probe(const FrameConst& F, V3 p) {
-    return scene_dist<SC, false>(F, p);
+__device__ __forceinline__ float dist_probe(const FrameConst& F, V3 p, Tally& cnt) {
+    return scene_dist<SC, false>(F, p, cnt);
 }
 template <int SC>
 __device__ __forceinline__ V3 mnormalize(V3 a) {
@@ -50,13 +50,12 @@ __device__ __forceinline__ V3 mnormalize(V3 a) {
 
 // common.frag:697-708 (tetrahedral gradient, h = 0.001)
 template <int SC>
-__device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, uint32_t& cnt) {
+__device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt) {
     const float h = 0.001f;
-    float d0 = dist_march<SC>(F, p + v3(h, -h, -h));
-    float d1 = dist_march<SC>(F, p + v3(-h, -h, h));
-    float d2 = dist_march<SC>(F, p + v3(-h, h, -h));
-    float d3 = dist_march<SC>(F, p + v3(h, h, h));
-    cnt += 4;
+    float d0 = dist_march<SC>(F, p + v3(h, -h, -h), cnt);
+    float d1 = dist_march<SC>(F, p + v3(-h, -h, h), cnt);
+    float d2 = dist_march<SC>(F, p + v3(-h, h, -h), cnt);
+    float d3 = dist_march<SC>(F, p + v3(h, h, h), cnt);
     V3 g = v3(d0, -d0, -d0) + v3(-d1, -d1, d1);
     g = g + v3(-d2, d2, -d2);
     g = g + v3(d3, d3, d3);
@@ -66,14 +65,13 @@ __device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, uint32_t& c
 // common.frag:879-901. Returns dist (depth on hit, -1 on miss, last SDF value
 // on step exhaustion) and the point whose SdResult is returned.
 template <int SC, bool INSIDE>
-__device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V3& last_q, uint32_t& cnt) {
+__device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V3& last_q, Tally& cnt) {
     float depth = ZNEAR;
     float res = 0.0f;
     last_q = ro;
     for (int i = 0; i < F.max_steps; i++) {
         V3 q = ro + rd * depth;
-        res = dist_march<SC>(F, q);
-        cnt++;
+        res = dist_march<SC>(F, q, cnt);
         last_q = q;
         if (INSIDE) {  // castRayDI, common.frag:903-925
             if (-res < 0.001f * depth) return depth;
@@ -89,12 +87,11 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
 
 // common.frag:931-954 (scene T marcher): returns the point
 template <int SC>
-__device__ __forceinline__ V3 cast_ray(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+__device__ __forceinline__ V3 cast_ray(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     float depth = ZNEAR;
     V3 p = ro + rd * depth;
     for (int i = 0; i < F.max_steps; i++) {
-        float dist = dist_march<SC>(F, p);
-        cnt++;
+        float dist = dist_march<SC>(F, p, cnt);
         if (dist < 0.001f) return p;
         depth += dist;
         p = ro + rd * depth;
@@ -106,14 +103,13 @@ __device__ __forceinline__ V3 cast_ray(const FrameConst& F, V3 ro, V3 rd, uint32
 // common.frag:810-831, k = 4
 template <int SC>
 __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
-                                              uint32_t& cnt) {
+                                              Tally& cnt) {
     const float k = 4.0f;
     float res = 1.0f, ph = 1e20f;
     int it = 0;
     for (float t = mint; t < maxt;) {
         if (F.shadow_max_steps > 0 && it++ >= F.shadow_max_steps) break;
-        float h = dist_probe<SC>(F, ro + rd * t);
-        cnt++;
+        float h = dist_probe<SC>(F, ro + rd * t, cnt);
         if (h < 0.001f) return 0.0f;
         float y = mdiv<SC>(h * h, 2.0f * ph);
         float d = msqrt<SC>(h * h - y * y);
@@ -131,17 +127,19 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // Candidates with t - y <= 0 (k d / 0: inf or NaN) or h^2 < y^2 (sqrt NaN)
 // never lower res, as GLSL min(res, x) = x < res ? x : res.  On the first step
 // ph = 1e20 makes y vanish: the candidate is k h / t (Q = 1, D = t below).
+// Per-lane loop with one exit test per condition; the occlusion result is
+// recovered after the loop from the last h (a lane leaves through t >= maxt
+// only with h >= 0.001).
 __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
-                                                uint32_t& cnt) {
+                                                Tally& cnt) {
     const float k2 = 16.0f;  // k = 4
-    float num = 1.0f, den = 1.0f, P = 0.0f;
+    float num = 1.0f, den = 1.0f, P = 0.0f, h = 1.0f;
     bool first = true;
     int it = 0;
     for (float t = mint; t < maxt;) {
         if (F.shadow_max_steps > 0 && it++ >= F.shadow_max_steps) break;
-        float h = menger<false>(at(s, t));
-        cnt++;
-        if (h < 0.001f) return 0.0f;
+        h = menger_at(s, t, cnt);
+        if (h < 0.001f) break;
         float h2 = h * h;
         float Q = first ? 1.0f : fmaf(P, P, -h2);
         float D = first ? t : fmaf(t, P, -h2);
@@ -154,33 +152,33 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
         first = false;
         t = fmaf(h, 0.1f, t + 0.001f);
     }
-    return __builtin_amdgcn_sqrtf(num * __builtin_amdgcn_rcpf(den));
+    return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(num * __builtin_amdgcn_rcpf(den));
 }
 
 // castRay (common.frag:931-954) for scene T in sponge space; returns the
-// depth of the point the reference returns (ZFAR on escape)
-__device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s, uint32_t& cnt) {
+// depth of the point the reference returns (ZFAR on escape).  depth < ZFAR
+// holds at a hit and after step exhaustion, so the escape value is set once,
+// after the loop.
+__device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s, Tally& cnt) {
     float depth = ZNEAR;
     for (int i = 0; i < F.max_steps; i++) {
-        float dist = menger<false>(at(s, depth));
-        cnt++;
-        if (dist < 0.001f) return depth;
+        float dist = menger_at(s, depth, cnt);
+        if (dist < 0.001f) break;
         depth += dist;
-        if (depth >= ZFAR) return ZFAR;
+        if (depth >= ZFAR) break;
     }
-    return depth;
+    return depth >= ZFAR ? ZFAR : depth;
 }
 
 // common.frag:850-866
 template <int SC>
-__device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, uint32_t& cnt) {
+__device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tally& cnt) {
     float sum = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         V3 p = pos + (n * (float)(i + 1)) * 0.2f;
-        sum += (1.0f / (float)(1 << i)) * dist_probe<SC>(F, p);
+        sum += (1.0f / (float)(1 << i)) * dist_probe<SC>(F, p, cnt);
     }
-    cnt += 4;
     // maxSum = sum_i 2^-i (i+1) 0.2, accumulated in f32 as the reference does
     float maxSum = 0.0f;
 #pragma unroll
@@ -208,7 +206,7 @@ __device__ __forceinline__ V3 shadow_pow(float sha) {
 
 // output_shader.frag:85-116
 template <int SC>
-__device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm, uint32_t& cnt) {
+__device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm, Tally& cnt) {
     float th = 0.0f;
     V3 nn = -norm;
     for (int i = 0; i < 32; i++) {
@@ -216,15 +214,14 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
         float sl = F.hash11[i];
         V3 rnd = normalize(hash33(nn + v3s(fi)) - v3s(0.5f));
         V3 dir = rnd - (nn * 2.0f) * fminf(0.0f, dot(rnd, nn));  // reflectVector (:70-73)
-        th += sl + dist_probe<SC>(F, pos + dir * sl);
+        th += sl + dist_probe<SC>(F, pos + dir * sl, cnt);
     }
-    cnt += 32;
     return clamp01(th * 0.03125f);
 }
 
 // output_shader.frag:127-176
 template <int SC>
-__device__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, uint32_t& cnt) {
+__device__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, Tally& cnt) {
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     V3 lightDir = normalize(Ld);
@@ -255,7 +252,7 @@ __device__ __forceinline__ float fresnel(float n2, V3 normal, V3 incident, float
 
 // output_shader.frag:246-262
 template <int SC>
-__device__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+__device__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
     if (dist > 0.0f) {
@@ -269,7 +266,7 @@ __device__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt
 
 // output_shader.frag:298-343 (MAX_REFRACTIONS 4); live only in test scene OG
 template <int SC>
-__device__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption, uint32_t& cnt) {
+__device__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption, Tally& cnt) {
     V3 color = v3s(0.0f);
     float invert = -1.0f;
     float absorb = 0.0f;
@@ -300,7 +297,7 @@ __device__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption
 
 // output_shader.frag:348-385
 template <int SC>
-__device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+__device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
     if (!(dist > 0.0f)) return background(ro, rd);
@@ -324,7 +321,7 @@ __device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
 }
 
 // template.frag:45-76 (scene T)
-__device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+__device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     constexpr int SC = SCENE_T;
     V3 p = ro + rd * cast_ray_T(F, sponge_ray(F, ro, rd), cnt);
     V3 n = normal_fast<SC>(F, p, cnt);
@@ -352,7 +349,7 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, uint32
 }
 
 // BASELINE config-1 scene S0: castRayD + normal + lambert
-__device__ __forceinline__ V3 render_S0(const FrameConst& F, V3 ro, V3 rd, uint32_t& cnt) {
+__device__ __forceinline__ V3 render_S0(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     constexpr int SC = SCENE_S0;
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);

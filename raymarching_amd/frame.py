@@ -4,8 +4,8 @@ Pixels are independent, so a frame shards by rows.  Rows are dealt to ranks
 in bands of ``band`` rows, round robin: rank r owns frame row y iff
 ``(y // band) % nshards == r`` (cheap sky rows and expensive sponge / floor
 rows spread evenly).  Each rank renders its rows packed in
-increasing y (``rm_render_band``), optionally packs them to RGBA8
-(``rm_pack_rgba8``), and one gather brings every band to the root, where
+increasing y (``rm_render_rows``, or ``rm_render_rows_rgba8``, whose kernel
+packs RGBA8 in its epilogue), and one gather brings every band to the root, where
 ``rm_deinterleave`` writes the frame.  The gather is the only collective on
 the path (``torch.distributed.gather``; the "nccl" backend is RCCL).
 
@@ -108,12 +108,11 @@ class DistributedFrame:
         self.nmine = self.plan.count(rank)
         chunks = max(1, min(int(chunks), rps))
         self.cuts = [round(c * rps / chunks) for c in range(chunks + 1)]
-        self.local = torch.empty((rps, W, 4), dtype=torch.float32, device=dev)
         nbuf = 2 if world > 1 else 1
-        if fmt == "rgba8":
-            self.wires = [torch.empty((rps, W), dtype=torch.int32, device=dev) for _ in range(nbuf)]
-        else:  # float4 renders straight into the slot being gathered
-            self.wires = [self.local] + [torch.empty_like(self.local) for _ in range(nbuf - 1)]
+        # the render kernel writes straight into the slot being gathered
+        shape = (rps, W) if fmt == "rgba8" else (rps, W, 4)
+        dtype = torch.int32 if fmt == "rgba8" else torch.float32
+        self.wires = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nbuf)]
         wire = self.wires[0]
         self.gathered = ([torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev) for _ in range(2)]
                          if rank == 0 and world > 1 else None)
@@ -127,10 +126,6 @@ class DistributedFrame:
         self.k = 0            # frames submitted
         self.pending = None   # (slot, [works]) of the frame whose gather is in flight
 
-    @property
-    def local8(self):
-        return self.wires[0] if self.fmt == "rgba8" else None
-
     def _pipelined(self):
         import torch.distributed as dist
         return self.world > 1 and dist.get_backend(self.group) != "gloo"
@@ -140,14 +135,11 @@ class DistributedFrame:
         j1 = min(j1, self.nmine)
         if j1 <= j0:
             return
-        dst = self.local if self.fmt == "rgba8" else self.wires[slot]
         if events is not None:
             events[0].record()
-        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, dst[j0:j1])
+        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, self.wires[slot][j0:j1])
         if events is not None:
             events[1].record()
-        if self.fmt == "rgba8":
-            self.r.pack_rgba8(self.local[j0:j1], out=self.wires[slot][j0:j1])
 
     def _gather_async(self, slot, j0, j1):
         import torch.distributed as dist
@@ -160,9 +152,10 @@ class DistributedFrame:
         self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered[slot], out=self.frame)
 
     def render_local(self, stats=False):
-        """This rank's rows only (no gather); stats: one synchronous launch."""
+        """This rank's rows only, into wire slot 0 (no gather); stats: one synchronous launch."""
         p = self.plan
-        return self.r.render_band(p.W, p.H, p.band, p.nshards, self.rank, out=self.local[: self.nmine], stats=stats)
+        return self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, 0, self.nmine,
+                                  self.wires[0][: self.nmine], stats=stats)
 
     def submit(self, events=None):
         """Enqueue one frame.  With N > 1 its gather stays in flight until the

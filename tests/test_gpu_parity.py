@@ -64,6 +64,24 @@ def test_hip_matches_reference_glsl_golden(R, path):
     assert_parity(m["scene"], img, o, label="vs oracle")
 
 
+# per-ray-step FLOP bounds of the instrumented tally (rm_device.h Tally,
+# SURVEY.md 8(d)): every term evaluated vs the reference's full tally
+FLOP_BOUNDS = {"S0": (9, 9), "T": (6 + 17, 155), "O": (18 + 17 + 16 + 1, 221), "OG": (18 + 17 + 16 + 1, 221)}
+
+
+@pytest.mark.parametrize("scene,pose", [("S0", None), ("T", "P0"), ("T", "P4"), ("O", "P0"), ("O", "P2"),
+                                        ("OG", "P3")])
+def test_flop_tally_within_reference_tally(R, scene, pose):
+    setup(R, scene, S0_POSE if scene == "S0" else POSES[pose], 128)
+    _, st = hip(R, 160, 96)
+    lo, hi = FLOP_BOUNDS[scene]
+    assert st["evals"] > 0
+    per = st["flop"] / st["evals"]
+    assert lo <= per <= hi, (scene, per)
+    if scene != "S0":
+        assert per < hi  # the early exits skip work somewhere in every such frame
+
+
 # ------------------------------------------------------- configs / poses
 
 
@@ -203,6 +221,34 @@ def test_render_rgba8_matches_pack(R, torch_cuda):
     st = rm.lib().rm_render_rgba8(R._ctx, 80, 60, R._ptr(host), None)
     assert st == 0
     np.testing.assert_array_equal(host.view(np.int32), a.cpu().numpy())
+
+
+@pytest.mark.parametrize("scene", ["S0", "T", "O", "OG"])
+def test_fused_rgba8_epilogue_bit_exact(R, torch_cuda, scene):
+    """The RGBA8 kernels (packing in the epilogue) equal rm_render + rm_pack_rgba8
+    bit for bit, for whole frames, bands and row sub-ranges, in every tiling,
+    and count the same ray-steps and FLOP."""
+    torch = torch_cuda
+    setup(R, scene, S0_POSE if scene == "S0" else POSES["P3"], 128)
+    W, H, band, n = 77, 45, 4, 3
+    full, sf = R.render(W, H, stats=True)
+    packed = R.pack_rgba8(full)
+    for k in ("tile8", "tile16", "tile16x4"):
+        R.set_params(kernel=k)
+        a, sa = R.render_rgba8(W, H, stats=True)
+        assert torch.equal(a, packed), k
+        assert (sa["evals"], sa["flop"]) == (sf["evals"], sf["flop"])
+    R.set_params(kernel="auto")
+    from raymarching_amd.frame import ShardPlan
+    plan = ShardPlan(W, H, band, n)
+    for s in range(n):
+        b = R.render_band_rgba8(W, H, band, n, s)
+        assert torch.equal(b, packed[plan.rows(s)])
+        part = torch.zeros_like(b)
+        c = b.shape[0]
+        R.render_rows(W, H, band, n, s, 0, c // 2, part[: c // 2])
+        R.render_rows(W, H, band, n, s, c // 2, c - c // 2, part[c // 2:])
+        assert torch.equal(part, b)
 
 
 def test_host_output_buffer(R, torch_cuda):

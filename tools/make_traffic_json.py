@@ -12,7 +12,7 @@ import os
 import sys
 
 summ, key = sys.argv[1], sys.argv[2]
-ksub = sys.argv[3] if len(sys.argv) > 3 else "rm_render_direct<1, false>"
+ksub = sys.argv[3] if len(sys.argv) > 3 else "rm_render_direct<1, false"
 out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
 d = json.load(open(summ))
 k = [n for n in d if ksub in n][0]
@@ -20,6 +20,9 @@ v = d[k]
 entry = {"kernel": k, "FETCH_SIZE_KiB": v["FETCH_SIZE"], "WRITE_SIZE_KiB": v["WRITE_SIZE"],
          "hbm_bytes_per_launch": (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024,
          "source": os.path.relpath(summ)}
+for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"):
+    if c in v:
+        entry[c] = v[c]
 allj = json.load(open(out)) if os.path.exists(out) else {}
 allj[key] = entry
 json.dump(allj, open(out, "w"), indent=1)

@@ -23,7 +23,8 @@ __global__ __launch_bounds__(256) void k(FrameConst F, int steps, float* out) {
     V3 rd = v3(0.01f, 0.02f, -1.0f);
     float acc = 0.0f, t = 0.0f;
     for (int i = 0; i < steps; i++) {
-        float d = scene_dist<SC, false>(F, ro + rd * t);
+        Tally n;
+        float d = scene_dist<SC, false>(F, ro + rd * t, n);
         acc += d;
         t += NEAR ? 0.0007f : 0.01f;
     }
