@@ -123,36 +123,33 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // softShadow2 for scene T (fast math), stepping in sponge space and free of
 // divisions and square roots.  With P = 2 ph the reference's y = h^2/P gives
 //   k sqrt(h^2 - y^2) / (t - y) = k h sqrt(P^2 - h^2) / (t P - h^2),
-// and res is kept squared as num/den, candidates compared by cross-products.
-// Candidates with t - y <= 0 (k d / 0: inf or NaN) or h^2 < y^2 (sqrt NaN)
-// never lower res, as GLSL min(res, x) = x < res ? x : res.  On the first step
-// ph = 1e20 makes y vanish: the candidate is k h / t (Q = 1, D = t below).
-// Per-lane loop with one exit test per condition; the occlusion result is
-// recovered after the loop from the last h (a lane leaves through t >= maxt
-// only with h >= 0.001).
+// and res^2 / k^2 is kept as num/den, candidates h^2 Q / D^2 compared by
+// cross-products (branch-free selects).  Candidates with t - y <= 0 (k d / 0:
+// inf or NaN) or h^2 < y^2 (sqrt NaN) never lower res, as GLSL
+// min(res, x) = x < res ? x : res.  On the first step ph = 1e20 makes y
+// vanish: the candidate is k h / t (Q = 1, D = t below).  The occlusion result
+// is recovered after the loop from the last h (a lane leaves through
+// t >= maxt only with h >= 0.001).
 __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                 Tally& cnt) {
-    const float k2 = 16.0f;  // k = 4
-    float num = 1.0f, den = 1.0f, P = 0.0f, h = 1.0f;
-    bool first = true;
-    int it = 0;
-    for (float t = mint; t < maxt;) {
-        if (F.shadow_max_steps > 0 && it++ >= F.shadow_max_steps) break;
+    float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
+    float t = mint;
+    // one exit test per step (occluded, t >= maxt, or the optional step cap);
+    // t grows by >= 0.001 per continuing step, NaN leaves
+    for (int it = 1; it == 1 ? t < maxt : true; it++) {
         h = menger_at(s, t, cnt);
-        if (h < 0.001f) break;
         float h2 = h * h;
-        float Q = first ? 1.0f : fmaf(P, P, -h2);
-        float D = first ? t : fmaf(t, P, -h2);
-        float cn = k2 * h2 * Q, cd = D * D;
-        if (D > 0.0f && Q >= 0.0f && cn * den < num * cd) {
-            num = cn;
-            den = cd;
-        }
-        P = 2.0f * h;
-        first = false;
+        float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
+        float D = it == 1 ? t : fmaf(t, P, -h2);
+        float cn = h2 * Q, cd = D * D;
+        bool upd = (D > 0.0f) & (Q >= 0.0f) & (cn * den < num * cd);
+        num = upd ? cn : num;
+        den = upd ? cd : den;
+        P = h + h;
         t = fmaf(h, 0.1f, t + 0.001f);
+        if ((h < 0.001f) | !(t < maxt) | (F.shadow_max_steps > 0 & it >= F.shadow_max_steps)) break;
     }
-    return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(num * __builtin_amdgcn_rcpf(den));
+    return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(16.0f * num * __builtin_amdgcn_rcpf(den));
 }
 
 // castRay (common.frag:931-954) for scene T in sponge space; returns the
@@ -163,9 +160,9 @@ __device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s
     float depth = ZNEAR;
     for (int i = 0; i < F.max_steps; i++) {
         float dist = menger_at(s, depth, cnt);
-        if (dist < 0.001f) break;
-        depth += dist;
-        if (depth >= ZFAR) break;
+        bool hit = dist < 0.001f;
+        depth = hit ? depth : depth + dist;
+        if (hit | (depth >= ZFAR)) break;  // one exit test per step
     }
     return depth >= ZFAR ? ZFAR : depth;
 }
