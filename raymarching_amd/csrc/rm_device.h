@@ -236,46 +236,56 @@ __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
     return len3<EXACT>(fmaxf(qx, 0.0f), fmaxf(qy, 0.0f), fmaxf(qz, 0.0f)) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f);
 }
 
+// scene O's sceneSDF distance (output_shader.frag:38-48) at world point p with
+// q = its sponge-space image (given by the caller: sponge_space(p), or the
+// sponge-space ray of a march)
+template <bool EXACT>
+__device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n) {
+    n.evals++;
+    float d3 = p.y;
+    float m, t2;
+    // Lower bounds of the sphere and the cube (Chebyshev <= Euclidean
+    // distance, exactly also after rounding), and sminCubic lowers the min
+    // by at most k/6: if even the bound of t1 is past the floor by more than
+    // the blend width, t2 = sminCubic(t1, plane) is exactly the plane.
+    float lb1 = fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))) - 1.0f;
+    float lb2 = fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f))) - 1.0f;
+    n.flop += FL_BOUNDS + FL_BOX + 1;
+    if (fminf(lb1, lb2) - 0.0834f >= d3 + 0.51f) {
+        t2 = d3;
+    } else {
+        n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
+        float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
+        float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+        float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
+        t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
+    }
+    // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width
+    // k = 0.33 (with a margin far above rounding), sminCubic's h is 0 and the
+    // result is exactly t2: the sponge's folds are not needed.
+    float mc = sponge_box(q);
+    if (mc >= t2 + 0.34f) return t2;
+    float d0 = sponge_folds<EXACT>(q, mc, n.flop);
+    n.flop += FL_SMIN;
+    return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
+}
+
 // Scene distances ("one ray-step" = one call).  EXACT keeps the GLSL's
 // roundings (scene O's marches and normals, whose results feed the normal
 // hash); the fast form serves every other call.
 template <int SC, bool EXACT>
 __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p, Tally& n) {
-    n.evals++;
     if constexpr (SC == SCENE_S0) {
+        n.evals++;
         n.flop += FL_SPHERE;
         return len3<EXACT>(p.x, p.y - 1.0f, p.z + 3.0f) - 1.0f;  // sphere(vec4(0,1,-3,1), p)
     } else if constexpr (SC == SCENE_T) {
+        n.evals++;
         n.flop += FL_TRANSFORM + FL_BOX;
         return menger<EXACT>(sponge_space<EXACT>(F, p), n.flop);  // template.frag:41 (repaired)
     } else {  // output_shader.frag:38-48
-        float d3 = p.y;
-        float m, t2;
-        // Lower bounds of the sphere and the cube (Chebyshev <= Euclidean
-        // distance, exactly also after rounding), and sminCubic lowers the min
-        // by at most k/6: if even the bound of t1 is past the floor by more than
-        // the blend width, t2 = sminCubic(t1, plane) is exactly the plane.
-        float lb1 = fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))) - 1.0f;
-        float lb2 = fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f))) - 1.0f;
-        n.flop += FL_BOUNDS + FL_TRANSFORM + FL_BOX + 1;
-        if (fminf(lb1, lb2) - 0.0834f >= d3 + 0.51f) {
-            t2 = d3;
-        } else {
-            n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
-            float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
-            float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
-            float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
-            t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
-        }
-        // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width
-        // k = 0.33 (with a margin far above rounding), sminCubic's h is 0 and the
-        // result is exactly t2: the sponge's folds are not needed.
-        V3 q = sponge_space<EXACT>(F, p);
-        float mc = sponge_box(q);
-        if (mc >= t2 + 0.34f) return t2;
-        float d0 = sponge_folds<EXACT>(q, mc, n.flop);
-        n.flop += FL_SMIN;
-        return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
+        n.flop += FL_TRANSFORM;
+        return scene_dist_O<EXACT>(p, sponge_space<EXACT>(F, p), n);
     }
 }
 

@@ -63,61 +63,55 @@ __device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt)
 }
 
 // common.frag:879-901. Returns dist (depth on hit, -1 on miss, last SDF value
-// on step exhaustion) and the point whose SdResult is returned.
+// on step exhaustion) and the point whose SdResult is returned.  One exit
+// test per step; at a hit depth is left as it was, so the hit flag and depth
+// give the three outcomes after the loop.
 template <int SC, bool INSIDE>
 __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V3& last_q, Tally& cnt) {
     float depth = ZNEAR;
     float res = 0.0f;
+    bool hit = false;
     last_q = ro;
     for (int i = 0; i < F.max_steps; i++) {
         V3 q = ro + rd * depth;
         res = dist_march<SC>(F, q, cnt);
         last_q = q;
         if (INSIDE) {  // castRayDI, common.frag:903-925
-            if (-res < 0.001f * depth) return depth;
-            depth -= res;
+            hit = -res < 0.001f * depth;
+            depth = hit ? depth : depth - res;
         } else {
-            if (res < 0.001f * depth) return depth;
-            depth += res;
+            hit = res < 0.001f * depth;
+            depth = hit ? depth : depth + res;
         }
-        if (depth >= ZFAR) return -1.0f;
+        if (hit | (depth >= ZFAR)) break;
     }
-    return res;
+    return hit ? depth : depth >= ZFAR ? -1.0f : res;
 }
 
-// common.frag:931-954 (scene T marcher): returns the point
-template <int SC>
-__device__ __forceinline__ V3 cast_ray(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
-    float depth = ZNEAR;
-    V3 p = ro + rd * depth;
-    for (int i = 0; i < F.max_steps; i++) {
-        float dist = dist_march<SC>(F, p, cnt);
-        if (dist < 0.001f) return p;
-        depth += dist;
-        p = ro + rd * depth;
-        if (depth >= ZFAR) return ro + rd * ZFAR;
-    }
-    return p;
-}
-
-// common.frag:810-831, k = 4
+// common.frag:810-831, k = 4, for scenes O/OG: the probes step along the
+// world ray and its sponge-space image, and the candidate is kept squared as
+// in soft_shadow2_T below (the shadow factor is smooth in its roundings).
 template <int SC>
 __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
                                               Tally& cnt) {
-    const float k = 4.0f;
-    float res = 1.0f, ph = 1e20f;
-    int it = 0;
-    for (float t = mint; t < maxt;) {
-        if (F.shadow_max_steps > 0 && it++ >= F.shadow_max_steps) break;
-        float h = dist_probe<SC>(F, ro + rd * t, cnt);
-        if (h < 0.001f) return 0.0f;
-        float y = mdiv<SC>(h * h, 2.0f * ph);
-        float d = msqrt<SC>(h * h - y * y);
-        res = fminf(res, mdiv<SC>(k * d, fmaxf(0.0f, t - y)));
-        ph = h;
-        t += h * 0.1f + 0.001f;
+    const LinRay w{ro, rd}, s = sponge_ray(F, ro, rd);
+    float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
+    float t = mint;
+    for (int it = 1; it == 1 ? t < maxt : true; it++) {
+        cnt.flop += FL_LINRAY;
+        h = scene_dist_O<false>(at(w, t), at(s, t), cnt);
+        float h2 = h * h;
+        float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
+        float D = it == 1 ? t : fmaf(t, P, -h2);
+        float cn = h2 * Q, cd = D * D;
+        bool upd = (D > 0.0f) & (Q >= 0.0f) & (cn * den < num * cd);
+        num = upd ? cn : num;
+        den = upd ? cd : den;
+        P = h + h;
+        t = fmaf(h, 0.1f, t + 0.001f);
+        if ((h < 0.001f) | !(t < maxt) | (F.shadow_max_steps > 0 & it >= F.shadow_max_steps)) break;
     }
-    return res;
+    return h < 0.001f ? 0.0f : sqrtf(16.0f * num / den);
 }
 
 // softShadow2 for scene T (fast math), stepping in sponge space and free of
