@@ -16,12 +16,19 @@
 //     the caller already holds (same p, pure function) and is reused.
 // All arithmetic is IEEE f32 (GLSL float).
 #pragma once
+#ifdef __HIPCC_RTC__  // compiled by hiprtc (scene plugins, rm_plugin.h)
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#else
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace rm {
 
-enum SceneId : int { SCENE_S0 = 0, SCENE_T = 1, SCENE_O = 2, SCENE_OG = 3 };
+// S0/T/O/OG are compiled in; SCENE_PLUGIN is a scene whose sceneSDF comes
+// from a HIP source file compiled at rm_load_scene time (rm_plugin.h)
+enum SceneId : int { SCENE_S0 = 0, SCENE_T = 1, SCENE_O = 2, SCENE_OG = 3, SCENE_PLUGIN = 4 };
 
 constexpr float ZNEAR = 0.02f;   // common.frag:13
 constexpr float ZFAR = 50.0f;    // common.frag:14
@@ -41,11 +48,23 @@ struct FrameConst {
     int row0;                      // first packed row of the shard this launch renders
     int max_steps;                 // MAX_MARCHING_STEPS (common.frag:15), run-time
     int shadow_max_steps;          // 0 = unbounded, as softshadow2 (common.frag:814)
+    float time;                    // u_time
+    float mouse_x, mouse_y;        // u_mouse
     float hash11[32];              // Hash11(i), i = 0..31 (output_shader.frag:54-59,102)
 };
 
+// A scene plugin's sceneSDF, bound in the plugin's translation unit
+// (rm_plugin.h) by specializing this for SCENE_PLUGIN: dist(p), mat(p), flop.
+template <int SC>
+struct PluginScene;
+
 // ------------------------------------------------------------- vec3 helpers
-struct V3 { float x, y, z; };
+struct V3 {
+    float x, y, z;
+    V3() = default;
+    __host__ __device__ constexpr V3(float x_, float y_, float z_) : x(x_), y(y_), z(z_) {}
+    __host__ __device__ constexpr explicit V3(float s) : x(s), y(s), z(s) {}
+};
 __device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
 __device__ __forceinline__ V3 v3s(float s) { return V3{s, s, s}; }
 __device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
@@ -283,6 +302,10 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p, Tally& n)
         n.evals++;
         n.flop += FL_TRANSFORM + FL_BOX;
         return menger<EXACT>(sponge_space<EXACT>(F, p), n.flop);  // template.frag:41 (repaired)
+    } else if constexpr (SC == SCENE_PLUGIN) {
+        n.evals++;
+        n.flop += PluginScene<SC>::flop;
+        return PluginScene<SC>::dist(p);
     } else {  // output_shader.frag:38-48
         n.flop += FL_TRANSFORM;
         return scene_dist_O<EXACT>(p, sponge_space<EXACT>(F, p), n);
@@ -291,13 +314,20 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p, Tally& n)
 
 // ------------------------------------------------------------- materials
 
+// struct Material (common.frag:20-35); the constructor takes the GLSL
+// constructor's arguments in order
 struct Mat {
     V3 diffuse, specular;
     float shininess, reflectivity, transparency;
     V3 absorption;
     float ior;
     V3 emission;
+    Mat() = default;
+    __device__ Mat(V3 d, V3 s, float sh, float refl, float tr, V3 ab, float ior_, V3 em)
+        : diffuse(d), specular(s), shininess(sh), reflectivity(refl), transparency(tr), absorption(ab), ior(ior_),
+          emission(em) {}
 };
+
 
 __device__ __forceinline__ Mat mat_make(V3 d, V3 s, float sh, float refl, float tr, V3 ab, float ior, V3 em) {
     Mat m;
@@ -352,6 +382,8 @@ __device__ __forceinline__ Mat scene_mat(const FrameConst& F, V3 p) {
         Mat mt2 = smin_mat(t1, mt1, d3, floor_mat(p), m2);
         (void)smin_cubic_d<true>(d0, t2, 0.33f, m3);
         return smin_mat(d0, mat_mirror(), t2, mt2, m3);
+    } else if constexpr (SC == SCENE_PLUGIN) {
+        return PluginScene<SC>::mat(p);
     } else {
         (void)F; (void)p;
         return mat_red();

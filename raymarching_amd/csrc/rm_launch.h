@@ -4,11 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "rm_device.h"
+#include "rm_render_direct.h"
 
 namespace rm {
 
-enum KernelKind : int { KERNEL_TILE16 = 0, KERNEL_TILE8 = 1, KERNEL_TILE16X4 = 2 };
 
 // out: W-wide rows of float4 (rgba8 = false) or RGBA8 words (rgba8 = true)
 hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,

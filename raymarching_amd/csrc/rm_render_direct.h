@@ -98,8 +98,12 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
     float t = mint;
     for (int it = 1; it == 1 ? t < maxt : true; it++) {
-        cnt.flop += FL_LINRAY;
-        h = scene_dist_O<false>(at(w, t), at(s, t), cnt);
+        if constexpr (SC == SCENE_PLUGIN) {
+            h = dist_probe<SC>(F, at(w, t), cnt);
+        } else {
+            cnt.flop += FL_LINRAY;
+            h = scene_dist_O<false>(at(w, t), at(s, t), cnt);
+        }
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
         float D = it == 1 ? t : fmaf(t, P, -h2);
@@ -301,7 +305,7 @@ __device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
         V3 r = reflect(rd, n);
         color = color + (render_reflection<SC>(F, p + r * 0.001f, r, cnt) * rf) * m.reflectivity;
     }
-    if constexpr (SC == SCENE_OG) {
+    if constexpr (SC == SCENE_OG || SC == SCENE_PLUGIN) {  // (scene O has no transparent material)
         if (m.transparency > 0.0f) {
             V3 r = refract(rd, n, 1.0f / m.ior);
             color = color + (render_refraction<SC>(F, p + r * 0.001f, r, m.absorption, cnt) * (1.0f - rf)) *
@@ -373,6 +377,61 @@ __device__ __forceinline__ void camera_ray(const FrameConst& F, int x, int y, fl
 __device__ __forceinline__ int shard_row(const FrameConst& F, int j) {
     int b = j / F.band, r = j - b * F.band;
     return (b * F.nshards + F.shard) * F.band + r;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int SC>
+__device__ __forceinline__ V3 render_pixel(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
+    if constexpr (SC == SCENE_S0) return render_S0(F, ro, rd, cnt);
+    else if constexpr (SC == SCENE_T) return render_T(F, ro, rd, cnt);
+    else return render_O<SC>(F, ro, rd, cnt);  // O, OG and plugins: output_shader.frag's render()
+}
+
+// Workgroup shapes (KernelKind): KERNEL_TILE16 = 16x16 pixels as 2x2 waves
+// of 8x8; KERNEL_TILE8 = one 8x8-pixel wave per workgroup (the dispatcher
+// then refills CUs at wave granularity, which shortens the tail of small or
+// uneven launches); KERNEL_TILE16X4 = one 16x4-pixel wave.
+enum KernelKind : int { KERNEL_TILE16 = 0, KERNEL_TILE8 = 1, KERNEL_TILE16X4 = 2 };
+template <int K> struct Tiling;
+template <> struct Tiling<KERNEL_TILE16> { static constexpr int TW = 16, TH = 16, WPB = 4, LW = 8; };
+template <> struct Tiling<KERNEL_TILE8> { static constexpr int TW = 8, TH = 8, WPB = 1, LW = 8; };
+template <> struct Tiling<KERNEL_TILE16X4> { static constexpr int TW = 16, TH = 4, WPB = 1, LW = 16; };
+
+// The body of a render launch: one lane per pixel of the workgroup's tile.
+// OUT = float4 (gl_FragColor) or uint32_t (RGBA8, packed in the epilogue, so
+// the displayed frame costs 4 B/px of HBM instead of 16 + 20 for a pack
+// pass).  COUNT: instrumented build, ray-steps and FLOP summed per wave into
+// evals[0..1].
+template <int SC, bool COUNT, int K, typename OUT>
+__device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict__ out,
+                                            unsigned long long* __restrict__ evals) {
+    using T = Tiling<K>;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int x = blockIdx.x * T::TW + (w & 1) * 8 + (lane % T::LW);
+    const int j = blockIdx.y * T::TH + (w >> 1) * 8 + (lane / T::LW);
+    Tally cnt;
+    if (x < F.W && j < F.nrows) {
+        const int y = shard_row(F, F.row0 + j);
+        float tcx, tcy;
+        V3 ro, rd;
+        camera_ray(F, x, y, tcx, tcy, ro, rd);
+        V3 c = render_pixel<SC>(F, ro, rd, cnt);
+        c = post_colour<FastMath<SC>::value>(c, tcx, tcy);
+        if constexpr (sizeof(OUT) == 4) out[(size_t)j * F.W + x] = pack_rgba8(c.x, c.y, c.z, 1.0f);
+        else out[(size_t)j * F.W + x] = make_float4(c.x, c.y, c.z, 1.0f);
+    }
+    if constexpr (COUNT) {
+        uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop);
+        if (lane == 0) {
+            atomicAdd(&evals[0], (unsigned long long)se);
+            atomicAdd(&evals[1], (unsigned long long)sf);
+        }
+    }
 }
 
 }  // namespace rm
