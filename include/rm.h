@@ -26,6 +26,7 @@
 #ifndef RM_H_
 #define RM_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -72,9 +73,27 @@ rm_status rm_destroy(rm_ctx *ctx);
  * The scene plugin is chosen by the file's base name: "output_shader.frag"
  * (scene O), "template.frag" (scene T, repaired as SURVEY.md App. A),
  * "sphere" (scene S0), "output_shader_glass" (test scene OG).  A registered
- * name needs no file on disk (the GPU host has no shader tree).  Unknown name
- * and no file -> RM_ERR_FILE; unknown name with a file -> RM_ERR_SCENE. */
+ * name needs no file on disk (the GPU host has no shader tree).  Any other
+ * existing file named "*.hip" is a scene plugin: a source defining
+ * `SdResult sceneSDF(vec3 p)` with the reference's scene library
+ * (common.frag:37-679; raymarching_amd/csrc/rm_sdf_lib.h), compiled here with
+ * hiprtc into output_shader.frag's pass around that scene (the reference's
+ * "Reload scene shader", main.cpp:134-139).  A compile error prints the log
+ * and returns RM_ERR_SCENE, keeping the previous scene.  Unknown name and no
+ * file -> RM_ERR_FILE; another existing file -> RM_ERR_SCENE. */
 rm_status rm_load_scene(rm_ctx *ctx, const char *file_name);
+
+/* Compile a scene plugin without loading it (no GPU needed), as a GL driver
+ * compiles a shader: RM_OK, RM_ERR_FILE (missing file or #include) or
+ * RM_ERR_SCENE (compile errors).  The compiler's log (NUL-terminated,
+ * truncated to log_size) goes to `log` when it is not NULL. */
+rm_status rm_compile_scene(const char *file_name, char *log, size_t log_size);
+
+/* sceneSDF(p) of the loaded scene at n points: points = n xyz float triples,
+ * dist = n floats, material = n x 16 floats of struct Material
+ * (common.frag:20-35, declaration order) or NULL.  Device or host pointers;
+ * returns when the results are written.  Uniforms (u_time ...) are the ctx's. */
+rm_status rm_scene_eval(rm_ctx *ctx, const float *points, int64_t n, float *dist, float *material);
 
 /* Replace sf::Shader::setUniform (include/SFML/Graphics/Shader.hpp:297,306,315)
  * for the names main.cpp sets: u_resolution (2f), u_pos (3f), u_mouse (2f),

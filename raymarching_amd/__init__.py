@@ -8,9 +8,10 @@ ShaderLoader / sf::Shader / RenderTexture surface plus the row-sharded
 multi-GPU frame (``frame.py``).
 """
 from ._lib import EXPORTS, LIB_PATH, RmError, lib  # noqa: F401
-from .api import Renderer, RenderTexture, Shader, ShaderLoader, shard_rows  # noqa: F401
+from .api import Renderer, RenderTexture, Shader, ShaderLoader, compile_scene, shard_rows  # noqa: F401
 from .poses import POSES, S0_POSE  # noqa: F401
 
 # ray-step (sceneSDF) algorithmic FLOP per scene: SURVEY.md 8(d), DESIGN.md
 FLOP_PER_EVAL = {"S0": 9, "T": 155, "O": 221, "OG": 221}
+SCENES_DIR = __import__("os").path.join(__import__("os").path.dirname(__file__), "scenes")  # plugin examples
 SCENE_FILES = {"S0": "sphere", "T": "template.frag", "O": "output_shader.frag", "OG": "output_shader_glass"}

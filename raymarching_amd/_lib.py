@@ -15,13 +15,15 @@ LIB_PATH = os.environ.get("RM_LIB") or os.path.join(HERE, "librm.so")
 RM_OK = 0
 STATUS = {0: "RM_OK", 1: "RM_ERR_INVALID_ARGUMENT", 2: "RM_ERR_FILE", 3: "RM_ERR_SCENE",
           4: "RM_ERR_NO_SCENE", 5: "RM_ERR_DEVICE", 6: "RM_ERR_OUT_OF_MEMORY"}
+STATUS_CODES = {v: k for k, v in STATUS.items()}
 
 # every symbol include/rm.h declares
 EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_set_uniform2f",
            "rm_set_uniform3f", "rm_set_params", "rm_get_params", "rm_set_stream", "rm_synchronize",
            "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8",
            "rm_pack_rgba8",
-           "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_last_error", "rm_status_string")
+           "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_last_error", "rm_status_string",
+           "rm_compile_scene", "rm_scene_eval")
 
 
 class RmParams(ctypes.Structure):
@@ -89,6 +91,8 @@ def lib() -> ctypes.CDLL:
         "rm_render_rows_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp,
                                   c.POINTER(RmStats)], c.c_int),
         "rm_fxaa": ([vp, c.c_int, c.c_int, vp, vp], c.c_int),
+        "rm_compile_scene": ([cp, vp, c.c_size_t], c.c_int),
+        "rm_scene_eval": ([vp, vp, c.c_int64, vp, vp], c.c_int),
         "rm_last_error": ([vp], cp),
         "rm_status_string": ([c.c_int], cp),
     }

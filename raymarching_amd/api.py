@@ -185,6 +185,18 @@ class Renderer:
         check(lib().rm_fxaa(self._ctx, W, H, self._ptr(frame8), self._ptr(out)), self._ctx)
         return out
 
+    def scene_eval(self, points, material: bool = False):
+        """sceneSDF(p) of the loaded scene at points [n, 3] (host, numpy):
+        dist [n], and with material=True also the [n, 16] Material floats."""
+        import numpy as np
+        pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+        n = len(pts)
+        dist = np.zeros(n, np.float32)
+        mat = np.zeros((n, 16), np.float32) if material else None
+        check(lib().rm_scene_eval(self._ctx, self._ptr(pts), n, self._ptr(dist),
+                                  self._ptr(mat) if material else None), self._ctx)
+        return (dist, mat) if material else dist
+
     def render_rgba8(self, W, H, out=None, stats=False):
         torch = _torch()
         if out is None:
@@ -195,6 +207,17 @@ class Renderer:
         check(lib().rm_render_rgba8(self._ctx, W, H, self._ptr(out), ctypes.byref(s) if stats else None),
               self._ctx)
         return (out, s.as_dict()) if stats else out
+
+
+def compile_scene(file_name: str):
+    """rm_compile_scene: compile a scene plugin with hiprtc, no GPU needed.
+    Returns (ok, log); a missing file or #include raises RmError."""
+    buf = ctypes.create_string_buffer(1 << 16)
+    st = lib().rm_compile_scene(file_name.encode(), ctypes.cast(buf, ctypes.c_void_p), len(buf))
+    log = buf.value.decode(errors="replace")
+    if st == _lib.STATUS_CODES["RM_ERR_FILE"]:
+        raise _lib.RmError(st, log)
+    return st == 0, log
 
 
 def _check_out(t, nfloats):

@@ -18,6 +18,7 @@
 #include <string>
 
 #include "rm_launch.h"
+#include "rm_plugin_host.h"
 
 using rm::FrameConst;
 
@@ -39,6 +40,7 @@ struct rm_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float4 *staging = nullptr;
     size_t staging_bytes = 0;
+    rmplugin::Module plugin;  // the loaded scene plugin (scene == SCENE_PLUGIN)
 };
 
 namespace {
@@ -108,6 +110,10 @@ int scene_of(const std::string &name) {
     return -1;
 }
 
+bool is_plugin_source(const std::string &file) {
+    return file.size() > 4 && file.compare(file.size() - 4, 4, ".hip") == 0;
+}
+
 inline float fract(float x) { return x - std::floor(x); }
 
 // output_shader.frag:54-59
@@ -146,6 +152,9 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int
     F.rx_c = std::cos(ax); F.rx_s = std::sin(ax);
     F.W = W; F.H = H;
     F.band = band; F.nshards = nshards; F.shard = shard; F.nrows = nrows;
+    F.time = c->time;
+    F.mouse_x = c->mouse[0];
+    F.mouse_y = c->mouse[1];
     F.max_steps = c->params.max_steps;
     F.shadow_max_steps = c->params.shadow_max_steps;
     for (int i = 0; i < 32; i++) F.hash11[i] = hash11((float)i);
@@ -186,7 +195,10 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     bool cnt = ctx->params.count_evals != 0;
     if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 2 * sizeof(unsigned long long), ctx->stream));
     if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-    hipError_t e = rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
+    hipError_t e =
+        ctx->scene == rm::SCENE_PLUGIN
+            ? rmplugin::launch_render(ctx->plugin, F, out, rgba8, cnt ? ctx->d_evals : nullptr, ctx->stream)
+            : rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) {
         RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
@@ -212,6 +224,8 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
     if ((long long)W * H > (1LL << 31)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: frame too large");
     if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
+    if (ctx->scene == rm::SCENE_PLUGIN && !ctx->plugin.render)
+        return fail(ctx, RM_ERR_SCENE, "scene plugin was compiled with RM_PLUGIN_EVAL_ONLY (no render kernel)");
     int n = rows_of_shard(H, band, nshards, shard);
     if (row_count < 0) row_count = n - row_begin;
     if (row_begin < 0 || row_count < 0 || row_begin + row_count > n)
@@ -262,6 +276,7 @@ rm_status rm_create(rm_ctx **out, int device) {
 rm_status rm_destroy(rm_ctx *ctx) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(ctx->device);
+    rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
     if (ctx->staging) (void)hipFree(ctx->staging);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -283,7 +298,21 @@ rm_status rm_load_scene(rm_ctx *ctx, const char *file_name) {
             std::fprintf(stderr, "%s\n", err.c_str());
             return fail(ctx, RM_ERR_FILE, err);
         }
-        if (sc < 0) return fail(ctx, RM_ERR_SCENE, "no HIP scene plugin for \"" + file + "\"");
+        if (sc < 0) {
+            if (!is_plugin_source(file)) return fail(ctx, RM_ERR_SCENE, "no HIP scene plugin for \"" + file + "\"");
+            // a scene plugin: compiled like the reference's shader reload; on
+            // failure the previous scene stays loaded
+            rmplugin::Code code;
+            std::string log;
+            if (!rmplugin::compile(src, file, code, log)) {
+                std::fprintf(stderr, "%s\n", log.c_str());
+                return fail(ctx, RM_ERR_SCENE, "scene plugin \"" + file + "\" failed to compile:\n" + log);
+            }
+            RM_HIP(hipSetDevice(ctx->device));
+            hipError_t e = rmplugin::load(code, ctx->plugin);
+            if (e != hipSuccess) return hip_fail(ctx, e, "scene plugin module load");
+            sc = rm::SCENE_PLUGIN;
+        }
     } else if (sc < 0) {
         std::string err = "ShaderLoader: can't load file \"" + file + "\"";
         std::fprintf(stderr, "%s\n", err.c_str());
@@ -436,6 +465,53 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) 
     hipError_t e = rm::launch_fxaa(in, out, W, H, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "fxaa launch");
     return RM_OK;
+}
+
+rm_status rm_scene_eval(rm_ctx *ctx, const float *points, int64_t n, float *dist, float *material) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (n < 0 || (n > 0 && (!points || !dist))) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_scene_eval: bad arguments");
+    if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
+    if (n == 0) return RM_OK;
+    RM_HIP(hipSetDevice(ctx->device));
+    // device views of the three buffers (host ones are staged)
+    const size_t pb = (size_t)n * 3 * sizeof(float), db = (size_t)n * sizeof(float), mb = (size_t)n * 16 * sizeof(float);
+    const bool dp = is_device_ptr(points), dd = is_device_ptr(dist), dm = !material || is_device_ptr(material);
+    char *tmp = nullptr;
+    if (!(dp && dd && dm)) RM_HIP(hipMalloc(&tmp, pb + db + (material ? mb : 0)));
+    const float *p = dp ? points : reinterpret_cast<float *>(tmp);
+    float *d = dd ? dist : reinterpret_cast<float *>(tmp + pb);
+    float *m = !material ? nullptr : dm ? material : reinterpret_cast<float *>(tmp + pb + db);
+    hipError_t e = hipSuccess;
+    if (!dp) e = hipMemcpyAsync(const_cast<float *>(p), points, pb, hipMemcpyHostToDevice, ctx->stream);
+    FrameConst F = frame_const(ctx, 1, 1, 1, 1, 0, 1);
+    if (e == hipSuccess)
+        e = ctx->scene == rm::SCENE_PLUGIN ? rmplugin::launch_eval(ctx->plugin, F, p, n, d, m, ctx->stream)
+                                           : rm::launch_scene_eval(ctx->scene, F, p, n, d, m, ctx->stream);
+    if (e == hipSuccess && !dd) e = hipMemcpyAsync(dist, d, db, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && material && !dm) e = hipMemcpyAsync(material, m, mb, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (tmp) (void)hipFree(tmp);
+    if (e != hipSuccess) return hip_fail(ctx, e, "rm_scene_eval");
+    return RM_OK;
+}
+
+rm_status rm_compile_scene(const char *file_name, char *log, size_t log_size) {
+    if (!file_name) return RM_ERR_INVALID_ARGUMENT;
+    std::string src, err, clog;
+    rm_status st = RM_OK;
+    if (!preprocess(file_name, src, err)) {
+        clog = err;
+        st = RM_ERR_FILE;
+    } else {
+        rmplugin::Code code;
+        if (!rmplugin::compile(src, file_name, code, clog)) st = RM_ERR_SCENE;
+    }
+    if (log && log_size > 0) {
+        size_t k = clog.size() < log_size - 1 ? clog.size() : log_size - 1;
+        std::memcpy(log, clog.data(), k);
+        log[k] = '\0';
+    }
+    return st;
 }
 
 const char *rm_last_error(rm_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }

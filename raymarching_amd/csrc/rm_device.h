@@ -65,13 +65,13 @@ struct V3 {
     __host__ __device__ constexpr V3(float x_, float y_, float z_) : x(x_), y(y_), z(z_) {}
     __host__ __device__ constexpr explicit V3(float s) : x(s), y(s), z(s) {}
 };
-__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 v3s(float s) { return V3{s, s, s}; }
-__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__host__ __device__ constexpr V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__host__ __device__ constexpr V3 v3s(float s) { return V3{s, s, s}; }
+__host__ __device__ constexpr V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__host__ __device__ constexpr V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__host__ __device__ constexpr V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__host__ __device__ constexpr V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__host__ __device__ constexpr V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ float length(V3 a) { return sqrtf(dot(a, a)); }
 __device__ __forceinline__ V3 normalize(V3 a) { return a * (1.0f / sqrtf(dot(a, a))); }
@@ -320,11 +320,11 @@ struct Mat {
     V3 diffuse, specular;
     float shininess, reflectivity, transparency;
     V3 absorption;
-    float ior;
+    float refraction_index;
     V3 emission;
     Mat() = default;
-    __device__ Mat(V3 d, V3 s, float sh, float refl, float tr, V3 ab, float ior_, V3 em)
-        : diffuse(d), specular(s), shininess(sh), reflectivity(refl), transparency(tr), absorption(ab), ior(ior_),
+    __host__ __device__ constexpr Mat(V3 d, V3 s, float sh, float refl, float tr, V3 ab, float ior_, V3 em)
+        : diffuse(d), specular(s), shininess(sh), reflectivity(refl), transparency(tr), absorption(ab), refraction_index(ior_),
           emission(em) {}
 };
 
@@ -332,7 +332,7 @@ struct Mat {
 __device__ __forceinline__ Mat mat_make(V3 d, V3 s, float sh, float refl, float tr, V3 ab, float ior, V3 em) {
     Mat m;
     m.diffuse = d; m.specular = s; m.shininess = sh; m.reflectivity = refl; m.transparency = tr;
-    m.absorption = ab; m.ior = ior; m.emission = em;
+    m.absorption = ab; m.refraction_index = ior; m.emission = em;
     return m;
 }
 __device__ __forceinline__ Mat mat_red() {  // output_shader.frag:12
@@ -358,7 +358,7 @@ __device__ __forceinline__ Mat floor_mat(V3 pos) {
 __device__ __forceinline__ Mat blend(const Mat& a, const Mat& b, float k) {
     return mat_make(mix3(a.diffuse, b.diffuse, k), mix3(a.specular, b.specular, k), gmix(a.shininess, b.shininess, k),
                     gmix(a.reflectivity, b.reflectivity, k), gmix(a.transparency, b.transparency, k),
-                    mix3(a.absorption, b.absorption, k), gmix(a.ior, b.ior, k), mix3(a.emission, b.emission, k));
+                    mix3(a.absorption, b.absorption, k), gmix(a.refraction_index, b.refraction_index, k), mix3(a.emission, b.emission, k));
 }
 __device__ __forceinline__ Mat smin_mat(float a, const Mat& ma, float b, const Mat& mb, float m) {
     return blend(ma, mb, a < b ? m : 1.0f - m);

@@ -58,6 +58,24 @@ hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, 
     }
 }
 
+#define RM_EVAL_LAUNCHER(name) \
+    hipError_t name(const FrameConst& F, const float* pts, long long n, float* dist, float* mat, hipStream_t s);
+RM_EVAL_LAUNCHER(launch_eval_s0)
+RM_EVAL_LAUNCHER(launch_eval_t)
+RM_EVAL_LAUNCHER(launch_eval_o)
+RM_EVAL_LAUNCHER(launch_eval_og)
+
+hipError_t launch_scene_eval(int scene, const FrameConst& F, const float* pts, long long n, float* dist, float* mat,
+                             hipStream_t s) {
+    switch (scene) {
+    case SCENE_S0: return launch_eval_s0(F, pts, n, dist, mat, s);
+    case SCENE_T: return launch_eval_t(F, pts, n, dist, mat, s);
+    case SCENE_O: return launch_eval_o(F, pts, n, dist, mat, s);
+    case SCENE_OG: return launch_eval_og(F, pts, n, dist, mat, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 template <typename E>
 static hipError_t deinterleave_t(const E* gathered, E* out, int W, int H, int band, int nshards, int rows_per_shard,
                                  hipStream_t s) {

@@ -16,6 +16,19 @@ __global__ __launch_bounds__(64 * Tiling<K>::WPB) void rm_render_direct(FrameCon
     render_tile<SC, COUNT, K, OUT>(F, out, evals);
 }
 
+template <int SC>
+__global__ __launch_bounds__(256) void rm_scene_eval(FrameConst F, const float* __restrict__ pts, long long n,
+                                                     float* __restrict__ dist, float* __restrict__ mat) {
+    scene_eval_one<SC>(F, pts, n, dist, mat);
+}
+
+template <int SC>
+hipError_t launch_eval(const FrameConst& F, const float* pts, long long n, float* dist, float* mat, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((rm_scene_eval<SC>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, pts, n, dist, mat);
+    return hipGetLastError();
+}
+
 template <int SC, int K, typename OUT>
 hipError_t launch_direct(const FrameConst& F, OUT* out, unsigned long long* evals, hipStream_t s) {
     using T = Tiling<K>;

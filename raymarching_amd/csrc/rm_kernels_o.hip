@@ -18,4 +18,13 @@ hipError_t launch_scene_og(const FrameConst& F, void* out, bool rgba8, unsigned 
     return launch_scene<SCENE_OG>(F, out, rgba8, evals, kernel, s);
 }
 
+hipError_t launch_eval_o(const FrameConst& F, const float* pts, long long n, float* dist, float* mat,
+                          hipStream_t s) {
+    return launch_eval<SCENE_O>(F, pts, n, dist, mat, s);
+}
+hipError_t launch_eval_og(const FrameConst& F, const float* pts, long long n, float* dist, float* mat,
+                          hipStream_t s) {
+    return launch_eval<SCENE_OG>(F, pts, n, dist, mat, s);
+}
+
 }  // namespace rm

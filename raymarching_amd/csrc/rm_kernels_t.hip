@@ -12,4 +12,13 @@ hipError_t launch_scene_t(const FrameConst& F, void* out, bool rgba8, unsigned l
     return launch_scene<SCENE_T>(F, out, rgba8, evals, kernel, s);
 }
 
+hipError_t launch_eval_s0(const FrameConst& F, const float* pts, long long n, float* dist, float* mat,
+                          hipStream_t s) {
+    return launch_eval<SCENE_S0>(F, pts, n, dist, mat, s);
+}
+hipError_t launch_eval_t(const FrameConst& F, const float* pts, long long n, float* dist, float* mat,
+                          hipStream_t s) {
+    return launch_eval<SCENE_T>(F, pts, n, dist, mat, s);
+}
+
 }  // namespace rm

@@ -12,6 +12,9 @@ namespace rm {
 // out: W-wide rows of float4 (rgba8 = false) or RGBA8 words (rgba8 = true)
 hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
                          hipStream_t s);
+// sceneSDF(p) of a compiled-in scene at n points (rm_scene_eval)
+hipError_t launch_scene_eval(int scene, const FrameConst& F, const float* pts, long long n, float* dist, float* mat,
+                             hipStream_t s);
 hipError_t launch_deinterleave(const float4* gathered, float4* out, int W, int H, int band, int nshards,
                                int rows_per_shard, hipStream_t s);
 hipError_t launch_deinterleave_u32(const uint32_t* gathered, uint32_t* out, int W, int H, int band, int nshards,

@@ -1,0 +1,40 @@
+// rm_plugin.h -- prelude of a scene plugin's translation unit.
+//
+// rm_load_scene("scene.hip") compiles, with hiprtc for gfx950,
+//
+//     #include "rm_plugin.h"
+//     namespace rm { namespace glsl {            // GLSL names win over HIP's
+//     #pragma clang force_cuda_host_device begin // GLSL has no __device__
+//     <the preprocessed scene source, GLSL spellings translated>
+//     #pragma clang force_cuda_host_device end
+//     } }
+//     #include "rm_plugin_kernels.h"
+//
+// The scene source defines `SdResult sceneSDF(vec3 p)` with the library of
+// rm_sdf_lib.h, as output_shader.frag:12-48 does with common.frag, and may
+// read the pass's uniforms u_resolution, u_pos, u_mouse, u_time
+// (common.frag:4-7).  The render pipeline is output_shader.frag's render()
+// and main() (rm_render_direct.h render_O), as for the compiled-in scene O.
+#pragma once
+#include "rm_render_direct.h"
+#include "rm_sdf_lib.h"
+
+namespace rm {
+namespace glsl {
+
+// Every plugin kernel takes the launch's FrameConst as its first argument:
+// the uniforms are read from the kernel-argument segment (scalar loads).
+typedef const __attribute__((address_space(4))) FrameConst* UniformPtr;
+__device__ __forceinline__ UniformPtr plugin_uniforms() {
+    return (UniformPtr)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
+}  // namespace glsl
+}  // namespace rm
+
+#define u_resolution (::rm::glsl::vec2(::rm::glsl::plugin_uniforms()->res_x, ::rm::glsl::plugin_uniforms()->res_y))
+#define u_pos                                                                                              \
+    (::rm::glsl::vec3(::rm::glsl::plugin_uniforms()->pos_x, ::rm::glsl::plugin_uniforms()->pos_y,          \
+                      ::rm::glsl::plugin_uniforms()->pos_z))
+#define u_mouse (::rm::glsl::vec2(::rm::glsl::plugin_uniforms()->mouse_x, ::rm::glsl::plugin_uniforms()->mouse_y))
+#define u_time (::rm::glsl::plugin_uniforms()->time)

@@ -1,0 +1,52 @@
+// rm_plugin_kernels.h -- epilogue of a scene plugin's translation unit
+// (rm_plugin.h): binds the scene's sceneSDF to the render pipeline and defines
+// the plugin's kernels, looked up by name (rm_plugin_host.cpp).  The first
+// argument of every kernel is the FrameConst the uniforms are read from.
+#pragma once
+
+template <>
+struct rm::PluginScene<rm::SCENE_PLUGIN> {
+#ifdef RM_SCENE_FLOP
+    static constexpr uint32_t flop = RM_SCENE_FLOP;  // per-ray-step FLOP, when the scene states it
+#else
+    static constexpr uint32_t flop = 0;
+#endif
+    __device__ static float dist(rm::V3 p) { return rm::glsl::sceneSDF(p).dist; }
+    __device__ static rm::Mat mat(rm::V3 p) { return rm::glsl::sceneSDF(p).mat; }
+};
+
+#ifndef RM_PLUGIN_EVAL_ONLY
+// output_shader.frag's pass over 8x8-pixel one-wave tiles.  One kernel serves
+// every launch: the output format and the instrumentation are run-time
+// arguments (a plugin compiles one pipeline instead of four).
+extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
+                                                                  unsigned long long* evals) {
+    using namespace rm;
+    const int lane = threadIdx.x;
+    const int x = blockIdx.x * 8 + (lane & 7), j = blockIdx.y * 8 + (lane >> 3);
+    Tally cnt;
+    if (x < F.W && j < F.nrows) {
+        const int y = shard_row(F, F.row0 + j);
+        float tcx, tcy;
+        V3 ro, rd;
+        camera_ray(F, x, y, tcx, tcy, ro, rd);
+        V3 c = post_colour<false>(render_pixel<SCENE_PLUGIN>(F, ro, rd, cnt), tcx, tcy);
+        const size_t i = (size_t)j * F.W + x;
+        if (rgba8) static_cast<uint32_t*>(out)[i] = pack_rgba8(c.x, c.y, c.z, 1.0f);
+        else static_cast<float4*>(out)[i] = make_float4(c.x, c.y, c.z, 1.0f);
+    }
+    if (evals) {
+        uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop);
+        if (lane == 0) {
+            atomicAdd(&evals[0], (unsigned long long)se);
+            atomicAdd(&evals[1], (unsigned long long)sf);
+        }
+    }
+}
+#endif
+
+// sceneSDF(p) at explicit points (rm_scene_eval)
+extern "C" __global__ __launch_bounds__(256) void rm_plugin_eval(rm::FrameConst F, const float* pts, long long n,
+                                                                 float* dist, float* mat) {
+    rm::scene_eval_one<rm::SCENE_PLUGIN>(F, pts, n, dist, mat);
+}

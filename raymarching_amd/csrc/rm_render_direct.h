@@ -280,7 +280,7 @@ __device__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption
         V3 ref = reflect(rd, n);
         color = color + light_O<SC>(F, m, ro, ref, p, n, g, cnt);
         if (invert > 0.0f) break;
-        float ior = invert < 0.0f ? m.ior : 1.0f / m.ior;
+        float ior = invert < 0.0f ? m.refraction_index : 1.0f / m.refraction_index;
         V3 raf = refract(rd, n, ior);
         bool tif = raf.x == 0.0f && raf.y == 0.0f && raf.z == 0.0f;
         rd = tif ? ref : raf;
@@ -300,14 +300,14 @@ __device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     V3 p = ro + rd * dist;
     V3 n = normal_fast<SC>(F, p, cnt);
     V3 color = light_O<SC>(F, m, ro, rd, p, n, n, cnt);
-    float rf = fresnel(m.ior, n, rd, m.transparency > 0.0f ? 0.0f : m.reflectivity);
+    float rf = fresnel(m.refraction_index, n, rd, m.transparency > 0.0f ? 0.0f : m.reflectivity);
     if (m.reflectivity > 0.0f) {
         V3 r = reflect(rd, n);
         color = color + (render_reflection<SC>(F, p + r * 0.001f, r, cnt) * rf) * m.reflectivity;
     }
     if constexpr (SC == SCENE_OG || SC == SCENE_PLUGIN) {  // (scene O has no transparent material)
         if (m.transparency > 0.0f) {
-            V3 r = refract(rd, n, 1.0f / m.ior);
+            V3 r = refract(rd, n, 1.0f / m.refraction_index);
             color = color + (render_refraction<SC>(F, p + r * 0.001f, r, m.absorption, cnt) * (1.0f - rf)) *
                                 m.transparency;
         }
@@ -390,6 +390,26 @@ __device__ __forceinline__ V3 render_pixel(const FrameConst& F, V3 ro, V3 rd, Ta
     if constexpr (SC == SCENE_S0) return render_S0(F, ro, rd, cnt);
     else if constexpr (SC == SCENE_T) return render_T(F, ro, rd, cnt);
     else return render_O<SC>(F, ro, rd, cnt);  // O, OG and plugins: output_shader.frag's render()
+}
+
+// sceneSDF(p) of the scene at n points (rm_scene_eval): the distance in the
+// reference's arithmetic (the EXACT form), and, when mat is set, the 16 floats
+// of struct Material (common.frag:20-35) in declaration order.
+template <int SC>
+__device__ __forceinline__ void scene_eval_one(const FrameConst& F, const float* pts, long long n, float* dist,
+                                               float* mat) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const V3 p = v3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+    Tally t;
+    dist[i] = scene_dist<SC, true>(F, p, t);
+    if (mat) {
+        const Mat m = scene_mat<SC>(F, p);
+        const float v[16] = {m.diffuse.x,    m.diffuse.y,    m.diffuse.z,    m.specular.x,    m.specular.y,  m.specular.z,
+                             m.shininess,    m.reflectivity, m.transparency, m.absorption.x,  m.absorption.y,
+                             m.absorption.z, m.refraction_index,          m.emission.x,   m.emission.y,    m.emission.z};
+        for (int k = 0; k < 16; k++) mat[16 * i + k] = v[k];
+    }
 }
 
 // Workgroup shapes (KernelKind): KERNEL_TILE16 = 16x16 pixels as 2x2 waves

@@ -36,6 +36,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, HERE)
 from raymarching_amd.poses import POSES, S0_POSE  # noqa: E402
 
 SS = "/usr/local/lib/python3.10/dist-packages/kaleido/executable/bin/swiftshader/"
@@ -132,16 +133,86 @@ def main_rewrite(s: str) -> str:
             "\to_col = vec4(col, 1.0);\n#endif" + tail)
 
 
-def scene_O(ref: str) -> str:
+def scene_O(ref: str, edit=None) -> str:
     s = preprocess(os.path.join(ref, "output_shader.frag"), ref)
+    if edit is not None:
+        s = edit(s)
     s = es3_rewrite(s)
-    s = must_sub("vec3(180, u_time * 2, 0)", "vec3(180, u_time * 2.0, 0)", s)
+    if edit is None or "u_time * 2, 0" in s:
+        s = must_sub("vec3(180, u_time * 2, 0)", "vec3(180, u_time * 2.0, 0)", s)
     s = must_sub("sd.mat.transparency > 0 ?", "sd.mat.transparency > 0.0 ?", s)
     s = must_sub("if (sd.mat.reflectivity > 0)", "if (sd.mat.reflectivity > 0.0)", s)
     s = must_sub("if (sd.mat.transparency > 0)", "if (sd.mat.transparency > 0.0)", s)
     s = must_sub("float reflectivity = 0.0)", "float reflectivity)", s)  # output_shader.frag:246
     s = count_hook(s, "SdResult sceneSDF(vec3 p)\n{")
     return HEADER + main_rewrite(s)
+
+
+def scene_MB(ref: str) -> str:
+    """output_shader.frag with the mandelbulb line it keeps commented out
+    (output_shader.frag:41) live in place of the Menger sponge (:42) -- the
+    scene raymarching_amd/scenes/mandelbulb.hip restates as a plugin."""
+    def edit(s):
+        s = must_sub("\t//SdResult dist0 = SdResult(mandelbulb(", "\tSdResult dist0 = SdResult(mandelbulb(", s, count=1)
+        return must_sub("\tSdResult dist0 = SdResult(mengersponge(", "\t//SdResult dist0 = SdResult(mengersponge(", s,
+                        count=1)
+    return scene_O(ref, edit)
+
+
+def scene_SC(ref: str) -> str:
+    """output_shader.frag with its sceneSDF replaced by the text of the
+    example plugin raymarching_amd/scenes/showcase.hip (written in the
+    GLSL subset both accept)."""
+    with open(os.path.join(os.path.dirname(os.path.dirname(HERE)), "raymarching_amd", "scenes", "showcase.hip")) as f:
+        scene = f.read()
+
+    def edit(s):
+        sig = "SdResult sceneSDF(vec3 p)\n{"
+        a = s.index(sig)
+        b = s.index("\n}\n", a) + 3
+        return s[:a] + scene + s[b:]
+    return scene_O(ref, edit)
+
+
+def lib_kat(ref: str) -> str:
+    """common.frag with the known-answer cases of lib_kat_cases.py: pixel
+    (x=i, y=fn) holds case fn at kat_point(i); POINTS_MODE writes the point."""
+    from lib_kat_cases import PRELUDE, kat_function
+    s = "#define ALLOW_MATERIAL_BLENDING\n#include \"common.frag\"\n" + PRELUDE + kat_function() + """
+SdResult sceneSDF(vec3 p)
+{
+	return r1(length(p) - 1.0);
+}
+void main()
+{
+	int i = int(gl_FragCoord.x);
+	int fn = int(gl_FragCoord.y);
+	vec3 p = kat_point(i);
+	SdResult r = kat(fn, p);
+#ifdef POINTS_MODE
+	o_col = vec4(p, r.dist);
+#else
+	o_col = vec4(r.dist, r.mat.diffuse);
+#endif
+}
+"""
+    s = _preprocess_text(s, ref)
+    s = es3_rewrite(s)
+    return HEADER + s
+
+
+def lib_kat_materials(ref: str) -> str:
+    """As lib_kat, writing the material of the case's SdResult instead:
+    pass k (0..3) writes floats 4k..4k+3 of the 16-float Material record
+    (diffuse, specular, shininess, reflectivity, transparency, absorption,
+    ior, emission -- rm_scene_eval's order)."""
+    s = lib_kat(ref)
+    return must_sub("\to_col = vec4(r.dist, r.mat.diffuse);",
+                    "\tMaterial m = r.mat;\n"
+                    "\tfloat f[16] = float[16](m.diffuse.x, m.diffuse.y, m.diffuse.z, m.specular.x, m.specular.y, "
+                    "m.specular.z, m.shininess, m.reflectivity, m.transparency, m.absorption.x, m.absorption.y, "
+                    "m.absorption.z, m.refraction_index, m.emission.x, m.emission.y, m.emission.z);\n"
+                    "\to_col = vec4(f[4 * KPASS], f[4 * KPASS + 1], f[4 * KPASS + 2], f[4 * KPASS + 3]);", s)
 
 
 def scene_T(ref: str) -> str:
@@ -421,6 +492,11 @@ FIXTURES = [
     ("O_96x54_P2", "O", 96, 54, "P2", 128),
     ("O_64_P6", "O", 64, 64, "P6", 128),
     ("O_72x40_P3_512", "O", 72, 40, "P3", 512),
+    # scene plugins (raymarching_amd/scenes/*.hip) against the same reference text
+    ("MB_64_P0", "MB", 64, 64, "P0", 128),
+    ("MB_72x40_P3", "MB", 72, 40, "P3", 128),
+    ("SC_64_P0", "SC", 64, 64, "P0", 128),
+    ("SC_96x54_P5", "SC", 96, 54, "P5", 128),
 ]
 
 
@@ -429,7 +505,7 @@ def main():
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--only", default=None)
     args = ap.parse_args()
-    builders = {"O": scene_O, "T": scene_T, "S0": scene_S0}
+    builders = {"O": scene_O, "T": scene_T, "S0": scene_S0, "MB": scene_MB, "SC": scene_SC}
     for name, scene, W, H, pose_name, steps in FIXTURES:
         if args.only and args.only not in name:
             continue
@@ -448,6 +524,24 @@ def main():
                             meta=json.dumps(meta))
         print(f"{name}: {dt:.2f}s mean={rgba[..., :3].mean():.4f} evals/px={cnt[..., 0].mean():.2f} "
               f"nan={int(np.isnan(rgba).sum())}")
+    # scene-library known answers (lib_kat_cases.py) for the plugin dialect
+    if not args.only or args.only in "LIB_kat":
+        from lib_kat_cases import CASES, N_POINTS
+        g = GL(N_POINTS, len(CASES))
+        noop = dict(pos=(0.0, 0.0, 0.0), mouse=(0.0, 0.0), time=0.0)
+        src = lib_kat(args.ref)
+        res = (N_POINTS, len(CASES))
+        pts = g.draw(g.program(src.replace("precision highp int;\n", "precision highp int;\n#define POINTS_MODE\n", 1)),
+                     noop, res)[::-1][0, :, :3].copy()
+        vals = g.draw(g.program(src), noop, res)[::-1].copy()
+        mats = np.concatenate([g.draw(g.program(lib_kat_materials(args.ref).replace(
+            "precision highp int;\n", f"precision highp int;\n#define KPASS {k}\n", 1)), noop, res)[::-1]
+            for k in range(4)], axis=-1)
+        meta = dict(cases=[c[0] for c in CASES], classes=[c[2] for c in CASES], renderer=g.renderer,
+                    generator="tests/golden/make_goldens.py (cases: tests/golden/lib_kat_cases.py)")
+        np.savez_compressed(os.path.join(HERE, "LIB_kat.npz"), points=pts, dist=vals[..., 0].copy(), mat=mats,
+                            meta=json.dumps(meta))
+        print(f"LIB_kat: {len(CASES)} cases x {N_POINTS} points, nan={int(np.isnan(vals).sum())}")
     # the FXAA post pass (post.frag), next to the hot path
     for name, img in fxaa_inputs():
         if args.only and args.only not in name:

@@ -28,6 +28,10 @@ POLICY = {
     "T": dict(f2e3=0.99, f1e2=0.995, mean=1e-3),
     "O": dict(f2e3=0.95, f1e2=0.99, mean=2e-3),
     "OG": dict(f2e3=0.95, f1e2=0.99, mean=2e-3),
+    # scene plugins (raymarching_amd/scenes): the mandelbulb's pow/atan/acos
+    # orbit is the most ulp-sensitive SDF of the library
+    "MB": dict(f2e3=0.9, f1e2=0.97, mean=5e-3),
+    "SC": dict(f2e3=0.95, f1e2=0.99, mean=2e-3),
 }
 
 

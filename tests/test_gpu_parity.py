@@ -15,7 +15,7 @@ from tests.parity import assert_parity, diff_stats
 pytestmark = pytest.mark.gpu
 
 GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
-                if not os.path.basename(p).startswith("FXAA_"))
+                if os.path.basename(p).startswith(("S0_", "T_", "O_")))
 
 
 @pytest.fixture(scope="module")
