@@ -22,19 +22,28 @@
 namespace rm {
 namespace glsl {
 
-// Every plugin kernel takes the launch's FrameConst as its first argument:
-// the uniforms are read from the kernel-argument segment (scalar loads).
-typedef const __attribute__((address_space(4))) FrameConst* UniformPtr;
-__device__ __forceinline__ UniformPtr plugin_uniforms() {
-    return (UniformPtr)__builtin_amdgcn_kernarg_segment_ptr();
+// The pass's uniforms, copied at the start of every plugin kernel from its
+// FrameConst argument into LDS, where any function of the scene can read
+// them (the kernel-argument segment is addressable only in the kernel's own
+// body, and hiprtc does not inline every call).
+struct PluginUniforms {
+    float res_x, res_y, pos_x, pos_y, pos_z, mouse_x, mouse_y, time;
+};
+__shared__ PluginUniforms plugin_lds_uniforms;
+
+__device__ __forceinline__ void plugin_bind_uniforms(const FrameConst& F) {
+    if (threadIdx.x == 0)
+        plugin_lds_uniforms = PluginUniforms{F.res_x, F.res_y, F.pos_x, F.pos_y, F.pos_z, F.mouse_x, F.mouse_y, F.time};
+    __syncthreads();
 }
+__device__ __forceinline__ const PluginUniforms& plugin_uniforms() { return plugin_lds_uniforms; }
 
 }  // namespace glsl
 }  // namespace rm
 
-#define u_resolution (::rm::glsl::vec2(::rm::glsl::plugin_uniforms()->res_x, ::rm::glsl::plugin_uniforms()->res_y))
-#define u_pos                                                                                              \
-    (::rm::glsl::vec3(::rm::glsl::plugin_uniforms()->pos_x, ::rm::glsl::plugin_uniforms()->pos_y,          \
-                      ::rm::glsl::plugin_uniforms()->pos_z))
-#define u_mouse (::rm::glsl::vec2(::rm::glsl::plugin_uniforms()->mouse_x, ::rm::glsl::plugin_uniforms()->mouse_y))
-#define u_time (::rm::glsl::plugin_uniforms()->time)
+#define u_resolution (::rm::glsl::vec2(::rm::glsl::plugin_uniforms().res_x, ::rm::glsl::plugin_uniforms().res_y))
+#define u_pos                                                                                            \
+    (::rm::glsl::vec3(::rm::glsl::plugin_uniforms().pos_x, ::rm::glsl::plugin_uniforms().pos_y,          \
+                      ::rm::glsl::plugin_uniforms().pos_z))
+#define u_mouse (::rm::glsl::vec2(::rm::glsl::plugin_uniforms().mouse_x, ::rm::glsl::plugin_uniforms().mouse_y))
+#define u_time (::rm::glsl::plugin_uniforms().time)

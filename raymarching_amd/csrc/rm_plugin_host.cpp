@@ -15,6 +15,8 @@
 #include <hip/hiprtc.h>
 
 #include <cctype>
+#include <cstdlib>
+#include <fstream>
 #include <map>
 #include <mutex>
 
@@ -188,12 +190,12 @@ std::string translation_unit(const std::string& src, const std::string& file) {
         name += c;
     }
     return "#include \"rm_plugin.h\"\n"
-           "namespace rm {\nnamespace glsl {\n"
+           "namespace rm {\nnamespace glsl {\nnamespace {\n"
            "#pragma clang force_cuda_host_device begin\n"
            "#line 1 \"" + name + "\"\n" +
            glsl_source(src) +
            "\n#pragma clang force_cuda_host_device end\n"
-           "}  // namespace glsl\n}  // namespace rm\n"
+           "}  // namespace\n}  // namespace glsl\n}  // namespace rm\n"
            "#include \"rm_plugin_kernels.h\"\n";
 }
 
@@ -238,6 +240,10 @@ bool compile(const std::string& src, const std::string& file, Code& code, std::s
     auto v = std::make_shared<std::vector<char>>(cs);
     hiprtcGetCode(prog, v->data());
     hiprtcDestroyProgram(&prog);
+    if (const char* dir = std::getenv("RM_PLUGIN_DUMP")) {  // debugging: the TU and its code object
+        std::ofstream(std::string(dir) + "/plugin_tu.hip") << tu;
+        std::ofstream(std::string(dir) + "/plugin.co", std::ios::binary).write(v->data(), (std::streamsize)cs);
+    }
     code = v;
     std::lock_guard<std::mutex> g(g_mu);
     g_cache[tu] = v;

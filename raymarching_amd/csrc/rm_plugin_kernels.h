@@ -1,7 +1,7 @@
 // rm_plugin_kernels.h -- epilogue of a scene plugin's translation unit
 // (rm_plugin.h): binds the scene's sceneSDF to the render pipeline and defines
 // the plugin's kernels, looked up by name (rm_plugin_host.cpp).  The first
-// argument of every kernel is the FrameConst the uniforms are read from.
+// argument of every kernel is the FrameConst the uniforms are bound from.
 #pragma once
 
 template <>
@@ -11,8 +11,8 @@ struct rm::PluginScene<rm::SCENE_PLUGIN> {
 #else
     static constexpr uint32_t flop = 0;
 #endif
-    __device__ static float dist(rm::V3 p) { return rm::glsl::sceneSDF(p).dist; }
-    __device__ static rm::Mat mat(rm::V3 p) { return rm::glsl::sceneSDF(p).mat; }
+    __device__ __forceinline__ static float dist(rm::V3 p) { return rm::glsl::sceneSDF(p).dist; }
+    __device__ __forceinline__ static rm::Mat mat(rm::V3 p) { return rm::glsl::sceneSDF(p).mat; }
 };
 
 #ifndef RM_PLUGIN_EVAL_ONLY
@@ -22,6 +22,7 @@ struct rm::PluginScene<rm::SCENE_PLUGIN> {
 extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
                                                                   unsigned long long* evals) {
     using namespace rm;
+    glsl::plugin_bind_uniforms(F);
     const int lane = threadIdx.x;
     const int x = blockIdx.x * 8 + (lane & 7), j = blockIdx.y * 8 + (lane >> 3);
     Tally cnt;
@@ -48,5 +49,6 @@ extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst
 // sceneSDF(p) at explicit points (rm_scene_eval)
 extern "C" __global__ __launch_bounds__(256) void rm_plugin_eval(rm::FrameConst F, const float* pts, long long n,
                                                                  float* dist, float* mat) {
+    rm::glsl::plugin_bind_uniforms(F);
     rm::scene_eval_one<rm::SCENE_PLUGIN>(F, pts, n, dist, mat);
 }

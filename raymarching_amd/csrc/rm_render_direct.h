@@ -216,7 +216,7 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
 
 // output_shader.frag:127-176
 template <int SC>
-__device__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, Tally& cnt) {
+__device__ __forceinline__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, Tally& cnt) {
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     V3 lightDir = normalize(Ld);
@@ -247,7 +247,7 @@ __device__ __forceinline__ float fresnel(float n2, V3 normal, V3 incident, float
 
 // output_shader.frag:246-262
 template <int SC>
-__device__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
+__device__ __forceinline__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
     if (dist > 0.0f) {
@@ -261,7 +261,7 @@ __device__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
 
 // output_shader.frag:298-343 (MAX_REFRACTIONS 4); live only in test scene OG
 template <int SC>
-__device__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption, Tally& cnt) {
+__device__ __forceinline__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption, Tally& cnt) {
     V3 color = v3s(0.0f);
     float invert = -1.0f;
     float absorb = 0.0f;
@@ -292,7 +292,7 @@ __device__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption
 
 // output_shader.frag:348-385
 template <int SC>
-__device__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
+__device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
     if (!(dist > 0.0f)) return background(ro, rd);

@@ -31,7 +31,11 @@ POLICY = {
     # scene plugins (raymarching_amd/scenes): the mandelbulb's pow/atan/acos
     # orbit is the most ulp-sensitive SDF of the library
     "MB": dict(f2e3=0.9, f1e2=0.97, mean=5e-3),
-    "SC": dict(f2e3=0.95, f1e2=0.99, mean=2e-3),
+    # showcase.hip: more lit surface under output_shader.frag's hashed
+    # sample vectors (fract(x * 443.897), :54-66) than scene O, so more
+    # pixels carry the ulp-amplified noise (measured 93.7 % within 2e-3,
+    # 99.98 % within 1e-2, mean 3e-4 on SC_64_P0)
+    "SC": dict(f2e3=0.92, f1e2=0.995, mean=1e-3),
 }
 
 
