@@ -198,7 +198,7 @@ def main():
         F = rm.FLOP_PER_EVAL[args.scene]
         flop_rank = st["flop"]
         ach = flop_rank / (kern / 1e3) / 1e12
-        out_bytes = W * fr.plan.count(0) * 16
+        out_bytes = W * fr.plan.count(0) * (4 if args.fmt == "rgba8" else 16)  # the frame the kernel writes
         pmc = {}
         try:
             pm = json.load(open(args.pmc))

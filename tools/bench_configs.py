@@ -36,7 +36,7 @@ def gpu_case(r, scene, W, H, steps, pose, band=None, nshards=1, reps=5):
         _, s2 = r.render_band(W, H, band, nshards, 0, out=buf, stats=True)
         ts.append(s2["kernel_ms"])
     ms = float(np.median(ts))
-    return st["evals"], ms, n
+    return st["evals"], st["flop"], ms, n
 
 
 def cpu_rate(scene, W, H, steps, pose, rows):
@@ -58,13 +58,14 @@ def main():
               ("O-4096", "O", 4096, 4096, 512, "P0", None, 1)]
     for name, scene, W, H, steps, pn, band, nsh in cases:
         pose = rm.S0_POSE if pn == "S0" else rm.POSES[pn]
-        evals, ms, n = gpu_case(r, scene, W, H, steps, pose, band, nsh)
+        evals, flop, ms, n = gpu_case(r, scene, W, H, steps, pose, band, nsh)
         rows = np.arange(0, H, max(1, H // 32), dtype=np.int32) if H > 64 else np.arange(H, dtype=np.int32)
         cpu = cpu_rate(scene, W, H, steps, pose, rows) if os.environ.get("NO_CPU") is None else None
         print(json.dumps(dict(config=name, scene=scene, W=W, H=H, max_steps=steps, pose=pn, rows=n,
                               kernel_ms=ms, ray_steps=evals, ray_steps_per_px=evals / (W * n),
                               ray_steps_per_s=evals / ms * 1e3, frames_per_s_share=1e3 / ms,
-                              tflops_alg=evals * F[scene] / ms / 1e9,
+                              tflops_counted=flop / ms / 1e9, flop_per_ray_step=flop / max(evals, 1),
+                              tflops_reference_tally=evals * F[scene] / ms / 1e9,
                               cpu_ray_steps_per_s=cpu, cpu_threads=oracle.lib(True).oracle_num_threads())),
               flush=True)
 
