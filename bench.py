@@ -118,6 +118,35 @@ def time_fxaa(r, frame8, stream, reps=20):
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": nbytes}
 
 
+def time_bloom(r, frame8, stream, reps=20):
+    """The reference's bloom pass (bloom.frag + its mip chain, main.cpp:212-214)
+    over the RGBA8 frame on rank 0.  Algorithmic HBM bytes: the frame read
+    twice (mip level 1, base tap) and written once, each mip level bloom.frag
+    reads (1..d2, d2 = floor(log2(0.05 H)) + 1) written once and read once."""
+    import math
+
+    import torch
+
+    H, W = frame8.shape
+    out = torch.empty_like(frame8)
+    r.bloom(frame8, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        r.bloom(frame8, out=out)
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    lod = math.log2(0.05 * H)
+    d2 = min(int(math.floor(lod)) + 1, int(math.log2(max(W, H)))) if lod > 0 else 0
+    mip_texels = sum(max(1, W >> k) * max(1, H >> k) for k in range(1, d2 + 1))
+    nbytes = 4 * (3 * W * H + 2 * mip_texels)
+    gbs = nbytes / (ms / 1e3) / 1e9
+    return {"name": "bloom (shaders/post/bloom.frag:14-43 + mip chain)", "ms": ms, "bound": "hbm",
+            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+            "algorithmic_bytes": nbytes, "mip_levels": d2, "texel_fetches_per_px": 4 * (1 + 25 * 2)}
+
+
 def main():
     args = parse()
     import torch
@@ -252,6 +281,7 @@ def main():
         }
         if fr.frame is not None and fr.fmt == "rgba8":
             res["post_pass"] = time_fxaa(r, fr.frame, stream)
+            res["bloom_pass"] = time_bloom(r, fr.frame, stream)
         if world == 1 and args.cpu_seconds > 0:
             res["cpu_baseline"] = cpu_baseline(args, pose, W, H, args.cpu_seconds)
         print(json.dumps(res), flush=True)

@@ -165,6 +165,16 @@ rm_status rm_render_rows_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards,
  * post.frag, the output is the input flipped vertically. */
 rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
 
+/* The reference's bloom post pass (shaders/post/bloom.frag:14-43, applied by
+ * PostBloom::apply, source/post_bloom.cpp:9-13, main.cpp:212-214) over an
+ * RGBA8 frame: the mip levels bloom.frag's textureLod reads are built on the
+ * device (glGenerateMipmap semantics, kept in a context scratch buffer), then
+ * the 25-tap trilinear bloom is added to the frame; RGBA8 out, alpha 1.  As in
+ * the shader, the output is flipped vertically (uv = (tc.x, 1 - tc.y)).
+ * in/out: W x H device buffers, row 0 first, in != out.  Asynchronous on the
+ * context's stream. */
+rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
+
 /* Message of the last failing call on ctx ("" if none). */
 const char *rm_last_error(rm_ctx *ctx);
 const char *rm_status_string(rm_status status);

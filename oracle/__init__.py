@@ -76,6 +76,13 @@ def lib(fast: bool = False) -> ctypes.CDLL:
             getattr(L, fn).restype = ctypes.c_float
         L.oracle_fxaa.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_fxaa.restype = ctypes.c_int
+        L.oracle_bloom.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_bloom.restype = ctypes.c_int
+        L.oracle_mip_down.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_mip_down.restype = ctypes.c_int
+        L.oracle_bloom_levels.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.oracle_bloom_levels.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         L.oracle_num_threads.restype = ctypes.c_int
         _LIBS[name] = L
@@ -148,3 +155,40 @@ def fxaa(img_u32):
     if rc:
         raise ValueError("oracle_fxaa failed")
     return out, outf
+
+
+def bloom_levels(W, H):
+    """(lod, d1, d2) of bloom.frag's textureLod for a W x H image."""
+    lod, d1, d2 = ctypes.c_float(), ctypes.c_int(), ctypes.c_int()
+    lib().oracle_bloom_levels(int(W), int(H), ctypes.byref(lod), ctypes.byref(d1), ctypes.byref(d2))
+    return lod.value, d1.value, d2.value
+
+
+def mip_down(img_u32):
+    """One glGenerateMipmap step: [h, w] RGBA8 -> [max(1, h/2), max(1, w/2)]."""
+    img = np.ascontiguousarray(img_u32, np.uint32)
+    h, w = img.shape
+    out = np.zeros((max(1, h >> 1), max(1, w >> 1)), np.uint32)
+    if lib().oracle_mip_down(w, h, img.ctypes.data, out.ctypes.data):
+        raise ValueError("oracle_mip_down failed")
+    return out
+
+
+def bloom(img_u32):
+    """bloom.frag over an [H, W] RGBA8 image -> (RGBA8 [H, W], [levels 1..d2])."""
+    img = np.ascontiguousarray(img_u32, np.uint32)
+    H, W = img.shape
+    _, _, d2 = bloom_levels(W, H)
+    dims, w, h = [], W, H
+    for _ in range(d2):
+        w, h = max(1, w >> 1), max(1, h >> 1)
+        dims.append((h, w))
+    mips = np.zeros(max(1, sum(a * b for a, b in dims)), np.uint32)
+    out = np.zeros((H, W), np.uint32)
+    if lib().oracle_bloom(W, H, img.ctypes.data, out.ctypes.data, mips.ctypes.data):
+        raise ValueError("oracle_bloom failed")
+    levels, off = [], 0
+    for h, w in dims:
+        levels.append(mips[off:off + h * w].reshape(h, w))
+        off += h * w
+    return out, levels

@@ -915,3 +915,152 @@ int oracle_fxaa(int W, int H, const uint32_t *in, uint32_t *out, float *out_f32)
         }
     return 0;
 }
+
+/* ---------------------------------------------------------------- bloom
+ * shaders/post/bloom.frag:14-43 over postTexture as PostBloom::apply
+ * (source/post_bloom.cpp:9-13) samples it after setSmooth(true) +
+ * generateMipmap() (main.cpp:212-214): MIN LINEAR_MIPMAP_LINEAR, MAG LINEAR,
+ * CLAMP_TO_EDGE.  Mip level k+1 (max(1, w>>1) x max(1, h>>1)) is the bilinear
+ * resample of level k at its texel centres in the 0..255 domain, rounded to
+ * nearest-even: SwiftShader's glGenerateMipmap bit for bit on the even-sized
+ * goldens (tests/test_bloom.py). */
+
+/* level k (w x h) -> level k+1 */
+int oracle_mip_down(int w, int h, const uint32_t *in, uint32_t *out) {
+    if (!in || !out || w <= 0 || h <= 0) return 1;
+    const int w1 = w > 1 ? w >> 1 : 1, h1 = h > 1 ? h >> 1 : 1;
+    const float sx = (float)w / (float)w1, sy = (float)h / (float)h1;
+    for (int y = 0; y < h1; y++) {
+        float v = ((float)y + 0.5f) * sy - 0.5f;
+        float fy = floorf(v), b = v - fy;
+        int y0 = (int)fy, y1 = y0 + 1;
+        y0 = y0 < 0 ? 0 : (y0 >= h ? h - 1 : y0);
+        y1 = y1 < 0 ? 0 : (y1 >= h ? h - 1 : y1);
+        for (int x = 0; x < w1; x++) {
+            float u = ((float)x + 0.5f) * sx - 0.5f;
+            float fx = floorf(u), a = u - fx;
+            int x0 = (int)fx, x1 = x0 + 1;
+            x0 = x0 < 0 ? 0 : (x0 >= w ? w - 1 : x0);
+            x1 = x1 < 0 ? 0 : (x1 >= w ? w - 1 : x1);
+            uint32_t t00 = in[(size_t)y0 * w + x0], t01 = in[(size_t)y0 * w + x1];
+            uint32_t t10 = in[(size_t)y1 * w + x0], t11 = in[(size_t)y1 * w + x1];
+            uint32_t r = 0;
+            for (int c = 0; c < 32; c += 8) {
+                float c00 = (float)((t00 >> c) & 255u), c01 = (float)((t01 >> c) & 255u);
+                float c10 = (float)((t10 >> c) & 255u), c11 = (float)((t11 >> c) & 255u);
+                float r0 = (1.0f - a) * c00 + a * c01, r1 = (1.0f - a) * c10 + a * c11;
+                float s = (1.0f - b) * r0 + b * r1;
+                r |= (uint32_t)lrintf(s) << c;
+            }
+            out[(size_t)y * w1 + x] = r;
+        }
+    }
+    return 0;
+}
+
+/* bilinear fetch of a level (w x h) at normalized (u, v), CLAMP_TO_EDGE */
+static vec3 tex_bilinear(const uint32_t *img, int w, int h, float u, float v) {
+    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    float fx = floorf(x), fy = floorf(y);
+    float a = x - fx, b = y - fy;
+    int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    x0 = x0 < 0 ? 0 : (x0 >= w ? w - 1 : x0);
+    x1 = x1 < 0 ? 0 : (x1 >= w ? w - 1 : x1);
+    y0 = y0 < 0 ? 0 : (y0 >= h ? h - 1 : y0);
+    y1 = y1 < 0 ? 0 : (y1 >= h ? h - 1 : y1);
+    const uint32_t t00 = img[(size_t)y0 * w + x0], t01 = img[(size_t)y0 * w + x1];
+    const uint32_t t10 = img[(size_t)y1 * w + x0], t11 = img[(size_t)y1 * w + x1];
+    float o[3];
+    for (int c = 0; c < 3; c++) {
+        const int s = 8 * c;
+        float c00 = (float)((t00 >> s) & 255u) * UNORM_K, c01 = (float)((t01 >> s) & 255u) * UNORM_K;
+        float c10 = (float)((t10 >> s) & 255u) * UNORM_K, c11 = (float)((t11 >> s) & 255u) * UNORM_K;
+        float r0 = (1.0f - a) * c00 + a * c01, r1 = (1.0f - a) * c10 + a * c11;
+        o[c] = (1.0f - b) * r0 + b * r1;
+    }
+    return v3(o[0], o[1], o[2]);
+}
+
+/* The levels bloom.frag reads: textureLod at lod = log2(0.05 * u_resolution.y)
+ * (bloom.frag:22, u_resolution = the image size, post_bloom.cpp:6) blends
+ * levels d1 = floor(lod) and d2 = d1 + 1, both clamped to the last level q
+ * (GL ES 3.0 3.8.10.4).  Returns 1 + d2, the number of levels used. */
+int oracle_bloom_levels(int W, int H, float *lod, int *d1, int *d2) {
+    int q = 0;
+    for (int m = W > H ? W : H; m > 1; m >>= 1) q++;
+    const float l = log2f(0.05f * (float)H);
+    int a = 0, b = 0;
+    if (l > 0.0f) {
+        a = (int)floorf(l);
+        a = a > q ? q : a;
+        b = a + 1 > q ? q : a + 1;
+    }
+    if (lod) *lod = l;
+    if (d1) *d1 = a;
+    if (d2) *d2 = b;
+    return b + 1;
+}
+
+/* bloom.frag:33-43 at output pixel (x, y); levels[k] is lw[k] x lh[k] */
+static uint32_t bloom_pixel(const uint32_t *const *levels, const int *lw, const int *lh, int W, int H, int x, int y,
+                            float lod, int d1, int d2) {
+    static const float G[3][3] = {{41.0f / 273.0f, 26.0f / 273.0f, 7.0f / 273.0f},
+                                  {26.0f / 273.0f, 16.0f / 273.0f, 4.0f / 273.0f},
+                                  {7.0f / 273.0f, 4.0f / 273.0f, 1.0f / 273.0f}};
+    const float tcx = ((float)x + 0.5f) / (float)W, tcy = ((float)y + 0.5f) / (float)H;
+    const float u = tcx, v = 1.0f - tcy; /* bloom.frag:36 */
+    vec3 color = tex_bilinear(levels[0], lw[0], lh[0], u, v);
+    const float scale = 0.05f, iaspect = (float)H / (float)W, fr = lod - floorf(lod);
+    vec3 bl = v3(0.0f, 0.0f, 0.0f);
+    for (int j = -2; j <= 2; j++)     /* bloom.frag:24-26 */
+        for (int i = -2; i <= 2; i++) {
+            const float uu = u + ((float)i * iaspect) * scale, vv = v + (float)j * scale;
+            vec3 s;
+            if (lod <= 0.0f) {
+                s = tex_bilinear(levels[0], lw[0], lh[0], uu, vv);
+            } else {
+                vec3 s1 = tex_bilinear(levels[d1], lw[d1], lh[d1], uu, vv);
+                vec3 s2 = tex_bilinear(levels[d2], lw[d2], lh[d2], uu, vv);
+                s = v3((1.0f - fr) * s1.x + fr * s2.x, (1.0f - fr) * s1.y + fr * s2.y,
+                       (1.0f - fr) * s1.z + fr * s2.z);
+            }
+            const float g = G[abs(i)][abs(j)];
+            bl = v3(bl.x + g * s.x, bl.y + g * s.y, bl.z + g * s.z);
+        }
+    color = v3(color.x + gmax(bl.x - 0.3f, 0.0f), color.y + gmax(bl.y - 0.3f, 0.0f),
+               color.z + gmax(bl.z - 0.3f, 0.0f)); /* bloom.frag:28,41 (intensity 1) */
+    return unorm8(color.x) | (unorm8(color.y) << 8) | (unorm8(color.z) << 16) | (255u << 24);
+}
+
+/* mips: optional buffer receiving levels 1..d2 packed one after the other
+ * (the HIP path's layout); NULL = internal scratch */
+int oracle_bloom(int W, int H, const uint32_t *in, uint32_t *out, uint32_t *mips) {
+    if (!in || !out || W <= 0 || H <= 0) return 1;
+    float lod;
+    int d1, d2;
+    const int nl = oracle_bloom_levels(W, H, &lod, &d1, &d2);
+    const uint32_t *levels[40];
+    int lw[40], lh[40];
+    size_t total = 0;
+    lw[0] = W;
+    lh[0] = H;
+    for (int k = 1; k < nl; k++) {
+        lw[k] = lw[k - 1] > 1 ? lw[k - 1] >> 1 : 1;
+        lh[k] = lh[k - 1] > 1 ? lh[k - 1] >> 1 : 1;
+        total += (size_t)lw[k] * lh[k];
+    }
+    uint32_t *buf = mips ? mips : (uint32_t *)malloc((total ? total : 1) * sizeof(uint32_t));
+    if (!buf) return 2;
+    levels[0] = in;
+    size_t off = 0;
+    for (int k = 1; k < nl; k++) {
+        oracle_mip_down(lw[k - 1], lh[k - 1], levels[k - 1], buf + off);
+        levels[k] = buf + off;
+        off += (size_t)lw[k] * lh[k];
+    }
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) out[(size_t)y * W + x] = bloom_pixel(levels, lw, lh, W, H, x, y, lod, d1, d2);
+    if (!mips) free(buf);
+    return 0;
+}

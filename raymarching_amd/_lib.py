@@ -22,7 +22,7 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_set_uniform3f", "rm_set_params", "rm_get_params", "rm_set_stream", "rm_synchronize",
            "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8",
            "rm_pack_rgba8",
-           "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_last_error", "rm_status_string",
+           "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_last_error", "rm_status_string",
            "rm_compile_scene", "rm_scene_eval")
 
 
@@ -91,6 +91,7 @@ def lib() -> ctypes.CDLL:
         "rm_render_rows_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp,
                                   c.POINTER(RmStats)], c.c_int),
         "rm_fxaa": ([vp, c.c_int, c.c_int, vp, vp], c.c_int),
+        "rm_bloom": ([vp, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_compile_scene": ([cp, vp, c.c_size_t], c.c_int),
         "rm_scene_eval": ([vp, vp, c.c_int64, vp, vp], c.c_int),
         "rm_last_error": ([vp], cp),

@@ -185,6 +185,15 @@ class Renderer:
         check(lib().rm_fxaa(self._ctx, W, H, self._ptr(frame8), self._ptr(out)), self._ctx)
         return out
 
+    def bloom(self, frame8, out=None):
+        """bloom.frag (with its mip chain) over an [H, W] RGBA8 (int32 words) device frame."""
+        torch = _torch()
+        H, W = frame8.shape
+        if out is None:
+            out = torch.empty_like(frame8)
+        check(lib().rm_bloom(self._ctx, W, H, self._ptr(frame8), self._ptr(out)), self._ctx)
+        return out
+
     def scene_eval(self, points, material: bool = False):
         """sceneSDF(p) of the loaded scene at points [n, 3] (host, numpy):
         dist [n], and with material=True also the [n, 16] Material floats."""

@@ -40,6 +40,8 @@ struct rm_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float4 *staging = nullptr;
     size_t staging_bytes = 0;
+    uint32_t *mips = nullptr;  // bloom's mip levels 1..d2
+    size_t mips_texels = 0;
     rmplugin::Module plugin;  // the loaded scene plugin (scene == SCENE_PLUGIN)
 };
 
@@ -279,6 +281,7 @@ rm_status rm_destroy(rm_ctx *ctx) {
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
     if (ctx->staging) (void)hipFree(ctx->staging);
+    if (ctx->mips) (void)hipFree(ctx->mips);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     delete ctx;
@@ -464,6 +467,26 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) 
     RM_HIP(hipSetDevice(ctx->device));
     hipError_t e = rm::launch_fxaa(in, out, W, H, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "fxaa launch");
+    return RM_OK;
+}
+
+rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!in || !out || W <= 0 || H <= 0 || in == out)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_bloom: bad arguments");
+    if (!is_device_ptr(in) || !is_device_ptr(out))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_bloom: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    const rm::BloomPlan plan = rm::bloom_plan(W, H);
+    if (plan.texels > ctx->mips_texels) {
+        if (ctx->mips) RM_HIP(hipFree(ctx->mips));
+        ctx->mips = nullptr;
+        ctx->mips_texels = 0;
+        RM_HIP(hipMalloc(&ctx->mips, plan.texels * sizeof(uint32_t)));
+        ctx->mips_texels = plan.texels;
+    }
+    hipError_t e = rm::launch_bloom(in, out, ctx->mips, plan, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "bloom launch");
     return RM_OK;
 }
 

@@ -22,4 +22,15 @@ hipError_t launch_deinterleave_u32(const uint32_t* gathered, uint32_t* out, int 
 hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStream_t s);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 
+// bloom.frag's textureLod level pair and the mip levels 1..d2 it needs,
+// packed one after the other in a scratch buffer of `texels` RGBA8 words
+struct BloomPlan {
+    float lod = 0.0f, fr = 0.0f;
+    int d1 = 0, d2 = 0;
+    int w[40] = {}, h[40] = {};
+    size_t offset[40] = {}, texels = 0;
+};
+BloomPlan bloom_plan(int W, int H);
+hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s);
+
 }  // namespace rm

@@ -445,6 +445,89 @@ class GL:
         return out[::-1].copy()
 
 
+    def bloom(self, prog, img_u32, res):
+        """bloom.frag over `img_u32` as PostBloom::apply sees postTexture after
+        setSmooth(true) + generateMipmap() (main.cpp:212-214): MIN
+        LINEAR_MIPMAP_LINEAR, MAG LINEAR, CLAMP_TO_EDGE, the mip chain built by
+        glGenerateMipmap.  Returns (output RGBA8 row 0 = tc.y 0.5/H, [mip levels
+        1.. as stored, row 0 = t 0.5/h])."""
+        gl = self.gl
+        H, W = img_u32.shape
+        src = ctypes.c_uint()
+        gl.glGenTextures(1, ctypes.byref(src))
+        gl.glActiveTexture(0x84C0)
+        gl.glBindTexture(0x0DE1, src)
+        for pname, val in ((0x2801, 0x2703), (0x2800, 0x2601), (0x2802, 0x812F), (0x2803, 0x812F)):
+            gl.glTexParameteri(0x0DE1, pname, val)
+        data = np.ascontiguousarray(img_u32, np.uint32)
+        gl.glTexImage2D(0x0DE1, 0, 0x8058, W, H, 0, 0x1908, 0x1401, data.ctypes.data_as(ctypes.c_void_p))
+        gl.glGenerateMipmap(0x0DE1)
+        mips = []
+        fbo = ctypes.c_uint()
+        gl.glGenFramebuffers(1, ctypes.byref(fbo))
+        gl.glBindFramebuffer(0x8D40, fbo)
+        k = 1
+        while True:
+            w, h = max(1, W >> k), max(1, H >> k)
+            gl.glFramebufferTexture2D(0x8D40, 0x8CE0, 0x0DE1, src, k)
+            assert gl.glCheckFramebufferStatus(0x8D40) == 0x8CD5
+            m = np.zeros((h, w), np.uint32)
+            gl.glReadPixels(0, 0, w, h, 0x1908, 0x1401, m.ctypes.data_as(ctypes.c_void_p))
+            mips.append(m)
+            if w == 1 and h == 1:
+                break
+            k += 1
+        dst = ctypes.c_uint()
+        gl.glGenTextures(1, ctypes.byref(dst))
+        gl.glBindTexture(0x0DE1, dst)
+        gl.glTexStorage2D(0x0DE1, 1, 0x8058, W, H)
+        gl.glFramebufferTexture2D(0x8D40, 0x8CE0, 0x0DE1, dst, 0)
+        assert gl.glCheckFramebufferStatus(0x8D40) == 0x8CD5
+        gl.glBindTexture(0x0DE1, src)
+        gl.glViewport(0, 0, W, H)
+        gl.glUseProgram(prog)
+        gl.glUniform2f(gl.glGetUniformLocation(prog, b"u_resolution"), float(res[0]), float(res[1]))
+        gl.glUniform1i(gl.glGetUniformLocation(prog, b"u_main_tex"), 0)
+        gl.glDrawArrays(0x0004, 0, 3)
+        gl.glFinish()
+        out = np.zeros((H, W), np.uint32)
+        gl.glReadPixels(0, 0, W, H, 0x1908, 0x1401, out.ctypes.data_as(ctypes.c_void_p))
+        assert gl.glGetError() == 0
+        return out[::-1].copy(), mips
+
+
+def post_bloom(ref: str) -> str:
+    """shaders/post/bloom.frag with the ES 3.00 header swap."""
+    with open(os.path.join(ref, "shaders", "post", "bloom.frag")) as f:
+        s = f.read()
+    s = re.sub(r"^\s*#version.*$", "", s, flags=re.M)
+    s = must_sub("gl_TexCoord[0]", "vec4(v_uv, 0.0, 0.0)", s)
+    s = must_sub("gl_FragColor = vec4(color, 1.0);", "o_col = vec4(color, 1.0);", s)
+    s = must_sub("vec2(x * iaspect, y)", "vec2(float(x) * iaspect, y)", s)  # implicit int -> float
+    return ("#version 300 es\nprecision highp float;\nprecision highp int;\nprecision highp sampler2D;\n"
+            "in vec2 v_uv;\nout vec4 o_col;\n" + s)
+
+
+def bloom_inputs():
+    """(name, H x W RGBA8) inputs: FXAA outputs of two ray-march goldens (the
+    reference's bloom input is post.frag's output) and synthetic bright
+    patterns at power-of-two and odd sizes."""
+    out = []
+    for nm in ("FXAA_T_64_P0", "FXAA_O_96x54_P2"):
+        z = np.load(os.path.join(HERE, nm + ".npz"), allow_pickle=False)
+        out.append(("BLOOM_" + nm[5:], z["output"]))
+    rng = np.random.default_rng(20261016)
+    for H, W in ((64, 128), (37, 61), (256, 256)):
+        yy, xx = np.mgrid[0:H, 0:W]
+        img = np.zeros((H, W, 4), np.float32)
+        img[..., 3] = 1.0
+        img[..., 0] = np.clip(1.2 - np.hypot(xx - W * 0.3, yy - H * 0.4) / (0.15 * H), 0, 1)   # a bright disc
+        img[..., 1] = ((xx // 7 + yy // 5) % 2) * 0.9                                        # blocks
+        img[..., 2] = rng.uniform(0, 1, (H, W))                                               # noise
+        out.append((f"BLOOM_synthetic_{W}x{H}", unorm8(img)))
+    return out
+
+
 def post_fxaa(ref: str) -> str:
     """post.frag (FXAA main, post.frag:135-144) with the ES 3.00 header swap."""
     with open(os.path.join(ref, "post.frag")) as f:
@@ -553,6 +636,20 @@ def main():
                     generator="tests/golden/make_goldens.py")
         np.savez_compressed(os.path.join(HERE, name + ".npz"), input=img, output=out, meta=json.dumps(meta))
         print(f"{name}: changed pixels {float(np.mean(out != img[::-1])):.3f}")
+    # the bloom post pass (shaders/post/bloom.frag) over its mip chain
+    for name, img in bloom_inputs():
+        if args.only and args.only not in name:
+            continue
+        H, W = img.shape
+        g = GL(W, H)
+        out, mips = g.bloom(g.program(post_bloom(args.ref)), img, (W, H))
+        meta = dict(pass_="shaders/post/bloom.frag", W=W, H=H, levels=len(mips) + 1,
+                    sampler="LINEAR_MIPMAP_LINEAR / LINEAR, CLAMP_TO_EDGE, glGenerateMipmap", renderer=g.renderer,
+                    generator="tests/golden/make_goldens.py")
+        arrs = {f"mip{k + 1}": m for k, m in enumerate(mips)}
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), input=img, output=out, meta=json.dumps(meta), **arrs)
+        print(f"{name}: levels {len(mips) + 1}, mean |out - in| "
+              f"{float(np.mean(np.abs((out & 255).astype(int) - (img[::-1] & 255).astype(int)))):.2f}")
 
 
 if __name__ == "__main__":
