@@ -23,12 +23,13 @@ hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStrea
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 
 // bloom.frag's textureLod level pair and the mip levels 1..d2 it needs,
-// packed one after the other in a scratch buffer of `texels` RGBA8 words
+// packed one after the other in a scratch buffer of `texels` 32-bit words
 struct BloomPlan {
     float lod = 0.0f, fr = 0.0f;
     int d1 = 0, d2 = 0;
     int w[40] = {}, h[40] = {};
     size_t offset[40] = {}, texels = 0;
+    size_t f4_offset = 0;  // lod > 0: levels d1, d2 as float4 (words from the buffer start)
 };
 BloomPlan bloom_plan(int W, int H);
 hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s);

@@ -96,7 +96,8 @@ def test_hip_bloom_bit_exact_vs_oracle(R, path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,H", [(1, 1), (7, 3), (33, 65), (1920, 1080), (4096, 16), (300, 2000)])
+@pytest.mark.parametrize("W,H", [(1, 1), (7, 3), (33, 65), (1920, 1080), (4096, 16), (16, 4096), (300, 2000),
+                                 (2048, 1152), (4096, 4096)])
 def test_hip_bloom_ragged_sizes(R, W, H):
     import torch
     rng = np.random.default_rng(W * 7919 + H)
