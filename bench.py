@@ -283,7 +283,7 @@ def main():
                             f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
                             f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0",
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
-                "band": args.band, "fmt": args.fmt, "kernel": args.kernel, "chunks": chunks,
+                "band": args.band, "fmt": args.fmt, "wire": fr.wire, "kernel": args.kernel, "chunks": chunks,
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
             },
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max,

@@ -145,6 +145,16 @@ rm_status rm_deinterleave(rm_ctx *ctx, int W, int H, int band, int nshards, int 
 rm_status rm_deinterleave_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
                                 const uint32_t *gathered, uint32_t *out);
 
+/* The 3 B/px wire of a row-sharded RGBA8 frame (the gather is
+ * the only exchange, so its bytes bound multi-GPU scaling).  The pass writes
+ * alpha 1 (vec4(col, 1.0), output_shader.frag:419, template.frag:98), so the
+ * wire carries RGB only: rm_pack_rgb8 drops the alpha byte of npixels RGBA8
+ * words; rm_deinterleave_rgb8 is rm_deinterleave_rgba8 over gathered rows of
+ * 3*W bytes, restoring alpha 255.  Device pointers, ctx stream. */
+rm_status rm_pack_rgb8(rm_ctx *ctx, int64_t npixels, const uint32_t *in, uint8_t *out);
+rm_status rm_deinterleave_rgb8(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
+                               const uint8_t *gathered, uint32_t *out);
+
 /* float RGBA -> RGBA8 unorm (round to nearest, clamped), device pointers. */
 rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t *out);
 

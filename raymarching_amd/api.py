@@ -153,8 +153,18 @@ class Renderer:
         return (out, s.as_dict()) if stats else out
 
     def deinterleave(self, W, H, band, nshards, rows_per_shard, gathered, out=None):
-        """gathered: [nshards, rows_per_shard, W, 4] f32 or [nshards, rows_per_shard, W] RGBA8 words."""
+        """gathered: [nshards, rows_per_shard, W, 4] f32, [nshards, rows_per_shard, W] RGBA8 words, or
+        [nshards, rows_per_shard, 3 * W] uint8 (the RGB8 wire; the frame is RGBA8 words, alpha 255)."""
         torch = _torch()
+        if gathered.dtype == torch.uint8:
+            if out is None:
+                out = torch.empty((H, W), dtype=torch.int32, device=gathered.device)
+            _check_out(out, H * W)
+            if gathered.numel() < nshards * rows_per_shard * W * 3 or not gathered.is_contiguous():
+                raise ValueError("deinterleave: RGB8 wire must be contiguous with 3*W bytes per row")
+            check(lib().rm_deinterleave_rgb8(self._ctx, W, H, band, nshards, rows_per_shard, self._ptr(gathered),
+                                             self._ptr(out)), self._ctx)
+            return out
         rgba8 = gathered.dtype != torch.float32  # RGBA8 words travel as int32
         per_px = 1 if rgba8 else 4
         if out is None:
@@ -164,6 +174,18 @@ class Renderer:
         _check_out(gathered, nshards * rows_per_shard * W * per_px)
         fn = lib().rm_deinterleave_rgba8 if rgba8 else lib().rm_deinterleave
         check(fn(self._ctx, W, H, band, nshards, rows_per_shard, self._ptr(gathered), self._ptr(out)), self._ctx)
+        return out
+
+    def pack_rgb8(self, frame8, out=None):
+        """RGBA8 words -> the 3 B/px RGB8 wire (alpha dropped; the pass writes alpha 1)."""
+        torch = _torch()
+        npx = frame8.numel()
+        if out is None:
+            out = torch.empty(tuple(frame8.shape[:-1]) + (3 * frame8.shape[-1],), dtype=torch.uint8,
+                              device=frame8.device)
+        if out.numel() < 3 * npx or out.dtype != torch.uint8 or not out.is_contiguous() or not frame8.is_contiguous():
+            raise ValueError("pack_rgb8: out must be a contiguous uint8 tensor with 3 bytes per pixel")
+        check(lib().rm_pack_rgb8(self._ctx, npx, self._ptr(frame8), self._ptr(out)), self._ctx)
         return out
 
     def pack_rgba8(self, frame, out=None):

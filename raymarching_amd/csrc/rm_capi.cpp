@@ -417,8 +417,9 @@ rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows) {
     return RM_OK;
 }
 
+// 0: float4, 1: RGBA8 words, 2: RGB8 wire -> RGBA8 words
 static rm_status deinterleave_any(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
-                                  const void *gathered, void *out, bool rgba8) {
+                                  const void *gathered, void *out, int kind) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (!gathered || !out || W <= 0 || H <= 0 || band <= 0 || nshards <= 0)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave: bad arguments");
@@ -428,7 +429,10 @@ static rm_status deinterleave_any(rm_ctx *ctx, int W, int H, int band, int nshar
     if (!is_device_ptr(gathered) || !is_device_ptr(out))
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave: device pointers required");
     RM_HIP(hipSetDevice(ctx->device));
-    hipError_t e = rgba8 ? rm::launch_deinterleave_u32(reinterpret_cast<const uint32_t *>(gathered),
+    hipError_t e = kind == 2 ? rm::launch_deinterleave_rgb8(reinterpret_cast<const uint8_t *>(gathered),
+                                                           reinterpret_cast<uint32_t *>(out), W, H, band, nshards,
+                                                           rows_per_shard, ctx->stream)
+                   : kind == 1 ? rm::launch_deinterleave_u32(reinterpret_cast<const uint32_t *>(gathered),
                                                       reinterpret_cast<uint32_t *>(out), W, H, band, nshards,
                                                       rows_per_shard, ctx->stream)
                          : rm::launch_deinterleave(reinterpret_cast<const float4 *>(gathered),
@@ -440,12 +444,29 @@ static rm_status deinterleave_any(rm_ctx *ctx, int W, int H, int band, int nshar
 
 rm_status rm_deinterleave(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard, const float *gathered,
                           float *out) {
-    return deinterleave_any(ctx, W, H, band, nshards, rows_per_shard, gathered, out, false);
+    return deinterleave_any(ctx, W, H, band, nshards, rows_per_shard, gathered, out, 0);
 }
 
 rm_status rm_deinterleave_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
                                 const uint32_t *gathered, uint32_t *out) {
-    return deinterleave_any(ctx, W, H, band, nshards, rows_per_shard, gathered, out, true);
+    return deinterleave_any(ctx, W, H, band, nshards, rows_per_shard, gathered, out, 1);
+}
+
+rm_status rm_deinterleave_rgb8(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard,
+                               const uint8_t *gathered, uint32_t *out) {
+    return deinterleave_any(ctx, W, H, band, nshards, rows_per_shard, gathered, out, 2);
+}
+
+rm_status rm_pack_rgb8(rm_ctx *ctx, int64_t npixels, const uint32_t *in, uint8_t *out) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (npixels == 0) return RM_OK;  // an empty shard (more shards than row bands)
+    if (!in || !out || npixels < 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_pack_rgb8: bad arguments");
+    if (!is_device_ptr(in) || !is_device_ptr(out))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_pack_rgb8: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_pack_rgb8(in, out, (size_t)npixels, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pack_rgb8 launch");
+    return RM_OK;
 }
 
 rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t *out) {

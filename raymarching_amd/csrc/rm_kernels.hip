@@ -5,6 +5,8 @@
 // the small frame kernels:
 //   rm_deinterleave              root-side permute of gathered row bands.
 //   rm_pack_rgba8                float4 -> RGBA8 (the reference target format).
+//   rm_pack_rgb8 / rm_deinterleave_rgb8   the 3 B/px wire of row-sharded RGBA8
+//                                frames (alpha is 1 by construction).
 // COUNT=true is the instrumented build used to count sceneSDF calls
 // (ray-steps); timing runs use COUNT=false.
 #include <hip/hip_runtime.h>
@@ -34,6 +36,56 @@ __global__ __launch_bounds__(256) void rm_pack_rgba8(const float4* __restrict__ 
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         float4 v = in[i];
         out[i] = pack_rgba8(v.x, v.y, v.z, v.w);
+    }
+}
+
+// RGBA8 words -> 3-byte RGB.  The pass writes gl_FragColor = vec4(col, 1.0)
+// (output_shader.frag:419, template.frag:98), so alpha carries no information
+// on the wire; the root restores it as 255.  vec: in 16-byte and out 4-byte
+// aligned, then 4 pixels per lane (one 16-byte load, three 4-byte stores).
+__global__ __launch_bounds__(256) void rm_pack_rgb8(const uint32_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      size_t n, int vec) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t ng = vec ? n / 4 : 0;
+    for (size_t g = t0; g < ng; g += stride) {
+        const uint4 v = reinterpret_cast<const uint4*>(in)[g];
+        uint32_t* o = reinterpret_cast<uint32_t*>(out) + 3 * g;
+        o[0] = (v.x & 0xFFFFFFu) | (v.y << 24);
+        o[1] = ((v.y >> 8) & 0xFFFFu) | (v.z << 16);
+        o[2] = ((v.z >> 16) & 0xFFu) | (v.w << 8);
+    }
+    for (size_t i = 4 * ng + t0; i < n; i += stride) {
+        const uint32_t w = in[i];
+        out[3 * i] = (uint8_t)w;
+        out[3 * i + 1] = (uint8_t)(w >> 8);
+        out[3 * i + 2] = (uint8_t)(w >> 16);
+    }
+}
+
+// gathered: nshards blocks of rows_per_shard packed rows of 3*W bytes; out:
+// the W x H RGBA8 frame (alpha 255).  vec (W % 4 == 0, aligned buffers): one
+// lane per 4 pixels (three 4-byte loads, one 16-byte store).
+__global__ __launch_bounds__(256) void rm_deinterleave_rgb8(const uint8_t* __restrict__ gathered,
+                                                              uint32_t* __restrict__ out, int W, int H, int band,
+                                                              int nshards, int rows_per_shard, int vec) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int per_row = vec ? W / 4 : W;
+    const size_t n = (size_t)per_row * H;
+    for (size_t i = t0; i < n; i += stride) {
+        const int y = (int)(i / per_row), xg = (int)(i - (size_t)y * per_row);
+        const int gb = y / band, r = y - gb * band;
+        const int shard = gb % nshards, lb = gb / nshards;
+        const size_t src_row = ((size_t)shard * rows_per_shard + lb * band + r) * 3 * W;  // bytes
+        if (vec) {
+            const uint32_t* s = reinterpret_cast<const uint32_t*>(gathered + src_row) + 3 * xg;
+            const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
+            reinterpret_cast<uint4*>(out + (size_t)y * W)[xg] =
+                make_uint4((w0 & 0xFFFFFFu) | 0xFF000000u, (w0 >> 24) | ((w1 & 0xFFFFu) << 8) | 0xFF000000u,
+                           (w1 >> 16) | ((w2 & 0xFFu) << 16) | 0xFF000000u, (w2 >> 8) | 0xFF000000u);
+        } else {
+            const uint8_t* s = gathered + src_row + 3 * (size_t)xg;
+            out[(size_t)y * W + xg] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | 0xFF000000u;
+        }
     }
 }
 
@@ -101,6 +153,27 @@ hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStrea
     if (!n) return hipSuccess;
     unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
     hipLaunchKernelGGL(rm_pack_rgba8, dim3(blocks), dim3(256), 0, s, in, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_rgb8(const uint32_t* in, uint8_t* out, size_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const int vec = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 4 == 0);
+    const size_t work = vec ? (n + 3) / 4 : n;
+    unsigned blocks = (unsigned)((work + 255) / 256 < 8192 ? (work + 255) / 256 : 8192);
+    hipLaunchKernelGGL(rm_pack_rgb8, dim3(blocks), dim3(256), 0, s, in, out, n, vec);
+    return hipGetLastError();
+}
+
+hipError_t launch_deinterleave_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
+                                    int rows_per_shard, hipStream_t s) {
+    const size_t n = (size_t)W * H;
+    if (!n) return hipSuccess;
+    const int vec = (W % 4 == 0) && ((uintptr_t)gathered % 4 == 0) && ((uintptr_t)out % 16 == 0);
+    const size_t work = vec ? n / 4 : n;
+    unsigned blocks = (unsigned)((work + 255) / 256 < 8192 ? (work + 255) / 256 : 8192);
+    hipLaunchKernelGGL(rm_deinterleave_rgb8, dim3(blocks), dim3(256), 0, s, gathered, out, W, H, band, nshards,
+                       rows_per_shard, vec);
     return hipGetLastError();
 }
 

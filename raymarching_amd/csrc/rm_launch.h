@@ -20,6 +20,9 @@ hipError_t launch_deinterleave(const float4* gathered, float4* out, int W, int H
 hipError_t launch_deinterleave_u32(const uint32_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
                                    int rows_per_shard, hipStream_t s);
 hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStream_t s);
+hipError_t launch_pack_rgb8(const uint32_t* in, uint8_t* out, size_t n, hipStream_t s);
+hipError_t launch_deinterleave_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
+                                    int rows_per_shard, hipStream_t s);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 
 // bloom.frag's textureLod level pair and the mip levels 1..d2 it needs,

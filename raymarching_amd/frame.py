@@ -84,8 +84,9 @@ class DistributedFrame:
 
     ``render()`` runs this rank's rows, gathers to rank 0 and (on rank 0)
     de-interleaves the frame; everything is asynchronous on the current
-    stream.  ``fmt`` is "rgba8" (the displayed RenderTexture format, 4 B/px on
-    the wire) or "float4" (full gl_FragColor, 16 B/px, used by parity tests).
+    stream.  ``fmt`` is "rgba8" (the displayed RenderTexture format; 3 B/px on
+    the wire, ``wire="rgb8"``, or 4 with ``wire="rgba8"``) or "float4" (full
+    gl_FragColor, 16 B/px, used by parity tests).
 
     Overlap of the gather (RCCL, xGMI) with rendering, two ways:
     * ``submit()`` / ``flush()`` pipeline consecutive frames: frame k's gather
@@ -97,10 +98,17 @@ class DistributedFrame:
       chunk k is gathered; it costs a launch tail per chunk.
     """
 
-    def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None, chunks=1):
+    def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None, chunks=1, wire="auto"):
         import torch
 
         self.r, self.rank, self.world, self.fmt, self.group = renderer, rank, world, fmt, group
+        # RGBA8 frames cross the wire as RGB8 (3 B/px: alpha is 1 by construction,
+        # rm_pack_rgb8); the root restores alpha while de-interleaving.
+        if wire == "auto":
+            wire = "rgb8" if fmt == "rgba8" and world > 1 else fmt
+        if wire not in (fmt, "rgb8") or (wire == "rgb8" and fmt != "rgba8"):
+            raise ValueError(f"wire {wire!r} does not carry {fmt!r} frames")
+        self.wire = wire
         # one shard: the packed rows are the frame rows (no de-interleave needed)
         self.plan = ShardPlan(W, H, band if world > 1 else H, world)
         dev = torch.device(f"cuda:{renderer.device}")
@@ -109,18 +117,23 @@ class DistributedFrame:
         chunks = max(1, min(int(chunks), rps))
         self.cuts = [round(c * rps / chunks) for c in range(chunks + 1)]
         nbuf = 2 if world > 1 else 1
-        # the render kernel writes straight into the slot being gathered
         shape = (rps, W) if fmt == "rgba8" else (rps, W, 4)
         dtype = torch.int32 if fmt == "rgba8" else torch.float32
-        self.wires = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nbuf)]
+        if self.wire == "rgb8":
+            # render into a local RGBA8 band, pack each chunk into the slot being gathered
+            self.local = torch.empty(shape, dtype=dtype, device=dev)
+            self.wires = [torch.empty((rps, 3 * W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        else:
+            # the render kernel writes straight into the slot being gathered
+            self.local = None
+            self.wires = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nbuf)]
         wire = self.wires[0]
         self.gathered = ([torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev) for _ in range(2)]
                          if rank == 0 and world > 1 else None)
         if world == 1:
-            self.frame = wire
+            self.frame = wire if self.local is None else self.local
         elif rank == 0:
-            shape = (H, W) if fmt == "rgba8" else (H, W, 4)
-            self.frame = torch.empty(shape, dtype=wire.dtype, device=dev)
+            self.frame = torch.empty((H, W) if fmt == "rgba8" else (H, W, 4), dtype=dtype, device=dev)
         else:
             self.frame = None
         self.k = 0            # frames submitted
@@ -135,11 +148,14 @@ class DistributedFrame:
         j1 = min(j1, self.nmine)
         if j1 <= j0:
             return
+        dst = self.wires[slot] if self.local is None else self.local
         if events is not None:
             events[0].record()
-        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, self.wires[slot][j0:j1])
+        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, dst[j0:j1])
         if events is not None:
             events[1].record()
+        if self.local is not None:
+            self.r.pack_rgb8(self.local[j0:j1], out=self.wires[slot][j0:j1])
 
     def _gather_async(self, slot, j0, j1):
         import torch.distributed as dist
@@ -154,8 +170,9 @@ class DistributedFrame:
     def render_local(self, stats=False):
         """This rank's rows only, into wire slot 0 (no gather); stats: one synchronous launch."""
         p = self.plan
-        return self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, 0, self.nmine,
-                                  self.wires[0][: self.nmine], stats=stats)
+        dst = self.wires[0] if self.local is None else self.local
+        return self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, 0, self.nmine, dst[: self.nmine],
+                                  stats=stats)
 
     def submit(self, events=None):
         """Enqueue one frame.  With N > 1 its gather stays in flight until the

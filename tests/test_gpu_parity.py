@@ -423,3 +423,91 @@ def test_render_rows_chunks_and_frame_pipeline(R, torch_cuda):
     fr = DistributedFrame(R, 80, 48, 16, 0, 1, fmt="rgba8", chunks=5)
     frame = fr.render()
     assert torch.equal(frame, R.render_rgba8(80, 48))
+
+
+@pytest.mark.parametrize("W,H,band,n", [(64, 48, 16, 2), (61, 50, 7, 3), (96, 64, 16, 8)])
+def test_rgb8_wire_reassembles_the_rgba8_frame(R, torch_cuda, W, H, band, n):
+    """rm_pack_rgb8 + rm_deinterleave_rgb8 (the 3 B/px wire) give the frame
+    rm_render_rgba8 gives, bit for bit; W % 4 != 0 takes the byte path."""
+    torch = torch_cuda
+    from raymarching_amd.frame import ShardPlan
+    setup(R, "T", POSES["P3"], 128)
+    R.set_params(count_evals=0)
+    full = R.render_rgba8(W, H)
+    plan = ShardPlan(W, H, band, n)
+    rps = plan.rows_per_shard
+    g = torch.zeros((n, rps, 3 * W), dtype=torch.uint8, device="cuda")
+    for s in range(n):
+        cnt = plan.count(s)
+        b = R.render_band_rgba8(W, H, band, n, s)
+        R.pack_rgb8(b, out=g[s, :cnt])
+        # the wire holds the RGB bytes of the band in pixel order
+        ref = b.cpu().numpy().view(np.uint8).reshape(cnt, W, 4)[..., :3].reshape(cnt, 3 * W)
+        assert np.array_equal(g[s, :cnt].cpu().numpy(), ref)
+    frame = R.deinterleave(W, H, band, n, rps, g)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full)
+    assert (frame.cpu().numpy().view(np.uint8).reshape(H, W, 4)[..., 3] == 255).all()
+
+
+def test_rgb8_pack_misaligned_and_ragged(R, torch_cuda):
+    """Unaligned sub-ranges (byte path) pack the same bytes as aligned ones."""
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    src = torch.from_numpy(rng.integers(-2 ** 31, 2 ** 31, 1031, dtype=np.int64).astype(np.int32)).cuda()
+    ref = src.cpu().numpy().view(np.uint8).reshape(-1, 4)[:, :3].reshape(-1)
+    out = torch.zeros(3 * 1031 + 8, dtype=torch.uint8, device="cuda")
+    R.pack_rgb8(src, out=out[:3 * 1031])
+    assert np.array_equal(out[:3 * 1031].cpu().numpy(), ref)
+    R.pack_rgb8(src[1:], out=out[1:1 + 3 * 1030])
+    torch.cuda.synchronize()
+    assert np.array_equal(out[1:1 + 3 * 1030].cpu().numpy(), ref[3:])
+
+
+def _frame_worker(rank, world, port, q):
+    import os as _os
+
+    import torch
+    import torch.distributed as dist
+
+    from raymarching_amd.frame import DistributedFrame
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = rm.Renderer(0)
+    setup(r, "T", POSES["P0"], 128)
+    r.set_params(count_evals=0)
+    fr = DistributedFrame(r, 96, 70, 8, rank, world, fmt="rgba8", chunks=2)
+    assert fr.wire == "rgb8"
+    for _ in range(2):
+        fr.submit()
+    frame = fr.flush()
+    if rank == 0:
+        torch.cuda.synchronize()
+        q.put(frame.cpu().numpy())
+    dist.barrier()
+    r.close()
+    dist.destroy_process_group()
+
+
+def test_distributed_frame_two_ranks_on_one_gpu(R, torch_cuda):
+    """Two ranks (gloo, both on cuda:0) through DistributedFrame's RGB8 wire:
+    rank 0's frame equals a one-rank rm_render_rgba8 frame."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_frame_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    setup(R, "T", POSES["P0"], 128)
+    R.set_params(count_evals=0)
+    ref = R.render_rgba8(96, 70).cpu().numpy()
+    assert np.array_equal(frame, ref)
