@@ -162,19 +162,24 @@ __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool 
     for (int m = 0; m < 3; m++) {
         if (!(active && d < INV[m])) return d;
         fl += FL_FOLD;
-        float hx = p.x * SH[m], hy = p.y * SH[m], hz = p.z * SH[m];
-        float ax = fmaf(2.0f, hx - floorf(hx), -1.0f);
-        float ay = fmaf(2.0f, hy - floorf(hy), -1.0f);
-        float az = fmaf(2.0f, hz - floorf(hz), -1.0f);
         float rx, ry, rz;
         if constexpr (EXACT) {
+            float hx = p.x * SH[m], hy = p.y * SH[m], hz = p.z * SH[m];
+            float ax = fmaf(2.0f, hx - floorf(hx), -1.0f);
+            float ay = fmaf(2.0f, hy - floorf(hy), -1.0f);
+            float az = fmaf(2.0f, hz - floorf(hz), -1.0f);
             rx = fabsf(1.0f - 3.0f * fabsf(ax));
             ry = fabsf(1.0f - 3.0f * fabsf(ay));
             rz = fabsf(1.0f - 3.0f * fabsf(az));
         } else {
-            rx = fabsf(fmaf(-3.0f, fabsf(ax), 1.0f));
-            ry = fabsf(fmaf(-3.0f, fabsf(ay), 1.0f));
-            rz = fabsf(fmaf(-3.0f, fabsf(az), 1.0f));
+            // |a| = |2 fract(x s/2) - 1| = 2 |g|, g = y - rint(y), y = x s/2 - 1/2:
+            // the distance from x s/2 to the nearest k + 1/2 (ties give 1/2 both
+            // ways).  4 VALU per axis (fma, rndne, sub, fma) instead of 5.
+            float yx = fmaf(p.x, SH[m], -0.5f), yy = fmaf(p.y, SH[m], -0.5f), yz = fmaf(p.z, SH[m], -0.5f);
+            float gx = yx - __builtin_rintf(yx), gy = yy - __builtin_rintf(yy), gz = yz - __builtin_rintf(yz);
+            rx = fabsf(fmaf(-6.0f, fabsf(gx), 1.0f));
+            ry = fabsf(fmaf(-6.0f, fabsf(gy), 1.0f));
+            rz = fabsf(fmaf(-6.0f, fabsf(gz), 1.0f));
         }
         float med = __builtin_amdgcn_fmed3f(rx, ry, rz);
         float c = EXACT ? div_const(med - 1.0f, S3[m], INV[m]) : fmaf(med, INV[m], -INV[m]);
