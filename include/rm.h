@@ -172,7 +172,7 @@ rm_status rm_render_rows_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards,
 /* The reference's FXAA post pass (post.frag:16-61, :135-144) over an RGBA8
  * frame: in/out W*H RGBA8 words (device, distinct), sampled as the reference's
  * RenderTexture is (nearest, clamp to edge), u_resolution = (W, H).  Like
- * post.frag, the output is the input flipped vertically. */
+ * post.frag, the output is the input flipped vertically.  W*H < 2^30. */
 rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
 
 /* The reference's bloom post pass (shaders/post/bloom.frag:14-43, applied by

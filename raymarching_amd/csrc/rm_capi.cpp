@@ -483,6 +483,8 @@ rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t 
 rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (!in || !out || W <= 0 || H <= 0 || in == out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_fxaa: bad arguments");
+    if ((int64_t)W * H >= ((int64_t)1 << 30))  // the kernel's 32-bit byte offsets
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_fxaa: frame of 2^30 texels or more");
     if (!is_device_ptr(in) || !is_device_ptr(out))
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_fxaa: device pointers required");
     RM_HIP(hipSetDevice(ctx->device));

@@ -12,8 +12,8 @@
 // Built without FMA contraction and with correctly rounded division (like
 // rm_kernels_o.hip) so the float path is bit-identical to the restatement in
 // oracle/rm_oracle.c; the nearest-texel choices then agree exactly too.
-// One thread per output pixel, 16x16-pixel workgroups (neighbour texels are
-// re-read from L1/L2; 4 B in + 4 B out of HBM per pixel).
+// Four pixels per lane, 64x16-pixel workgroups (neighbour texels are re-read
+// from L1/L2; 4 B in + 4 B out of HBM per pixel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,12 +26,19 @@ struct RGB { float r, g, b; };
 __device__ __forceinline__ float gmin_(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gmax_(float x, float y) { return x < y ? y : x; }
 
+// NEAREST + CLAMP_TO_EDGE fetch.  Each clamp is one v_med3_i32, and the load
+// takes a 32-bit byte offset from the uniform base (the saddr form, no 64-bit
+// address math; rm_fxaa rejects frames of 2^30 texels or more).
+__device__ __forceinline__ int clamp_med3(int v, int hi) {
+    int r;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "v"(hi));
+    return r;
+}
 __device__ __forceinline__ uint32_t texel(const uint32_t* __restrict__ img, int W, int H, float u, float v) {
-    int x = (int)floorf(u * (float)W);
-    int y = (int)floorf(v * (float)H);
-    x = x < 0 ? 0 : (x >= W ? W - 1 : x);
-    y = y < 0 ? 0 : (y >= H ? H - 1 : y);
-    return img[(size_t)y * W + x];
+    const int x = clamp_med3((int)floorf(u * (float)W), W - 1);
+    const int y = clamp_med3((int)floorf(v * (float)H), H - 1);
+    const uint32_t off = (uint32_t)(y * W + x) * 4u;
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(img) + off);
 }
 
 __device__ __forceinline__ RGB rgb(uint32_t t) {
@@ -47,11 +54,7 @@ __device__ __forceinline__ uint32_t unorm8(float c) {
     return (uint32_t)__float2int_rn(c * 255.0f);
 }
 
-__global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                       int W, int H) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
+__device__ __forceinline__ uint32_t fxaa_px(const uint32_t* __restrict__ in, int W, int H, int x, int y) {
     const float FXAA_REDUCE_MIN = 1.0f / 128.0f, FXAA_REDUCE_MUL = 1.0f / 8.0f, FXAA_SPAN_MAX = 8.0f;
     // post.frag:138: uv = vec2(gl_TexCoord.x, 1 - gl_TexCoord.y)
     const float fx = ((float)x + 0.5f) / (float)W;
@@ -83,12 +86,34 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
     float lB = luma(b);
     RGB c = (lB < lMin || lB > lMax) ? a : b;
     float alpha = (float)(tM >> 24) * (1.0f / 255.0f);
-    out[(size_t)y * W + x] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | (unorm8(alpha) << 24);
+    return unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | (unorm8(alpha) << 24);
+}
+
+// One lane per 4 pixels (rows y, y+4, y+8, y+12 of a 64x16-pixel workgroup
+// tile): the kernel is latency-bound (two dependent rounds of L2 taps per
+// pixel), so each lane keeps four pixels' taps in flight at once.
+constexpr int FXAA_TX = 64, FXAA_TY = 16, FXAA_PX = 4;
+__global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       int W, int H) {
+    const int x = blockIdx.x * FXAA_TX + (threadIdx.x & 63);
+    const int y0 = blockIdx.y * FXAA_TY + (threadIdx.x >> 6);
+    if (x >= W) return;
+    uint32_t r[FXAA_PX];
+#pragma unroll
+    for (int k = 0; k < FXAA_PX; k++) {
+        const int y = y0 + 4 * k;
+        r[k] = fxaa_px(in, W, H, x, y < H ? y : H - 1);  // straight-line: the four pixels' taps overlap
+    }
+#pragma unroll
+    for (int k = 0; k < FXAA_PX; k++) {
+        const int y = y0 + 4 * k;
+        if (y < H) out[(size_t)y * W + x] = r[k];
+    }
 }
 
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s) {
     if (W <= 0 || H <= 0) return hipSuccess;
-    dim3 grid((W + 15) / 16, (H + 15) / 16);
+    dim3 grid((W + FXAA_TX - 1) / FXAA_TX, (H + FXAA_TY - 1) / FXAA_TY);
     hipLaunchKernelGGL(rm_fxaa_kernel, grid, dim3(256), 0, s, in, out, W, H);
     return hipGetLastError();
 }
