@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--chunks", type=int, default=None,
                     help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
+    ap.add_argument("--streams", type=int, default=None, choices=[1, 2],
+                    help="HIP streams frames alternate on (default: 2 for N > 1 over RCCL, else 1)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "tile16", "tile8"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
@@ -191,7 +193,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream)
     chunks = args.chunks if args.chunks is not None else 1
-    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks)
+    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks, streams=args.streams)
 
     # instrumented run: ray-steps of this rank's rows, summed over ranks
     r.set_params(count_evals=1)
@@ -283,7 +285,7 @@ def main():
                             f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
                             f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0",
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
-                "band": args.band, "fmt": args.fmt, "wire": fr.wire, "kernel": args.kernel, "chunks": chunks,
+                "band": args.band, "fmt": args.fmt, "wire": fr.wire, "streams": len(fr.streams), "kernel": args.kernel, "chunks": chunks,
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
             },
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max,

@@ -83,22 +83,31 @@ class DistributedFrame:
     """One rank's share of a row-sharded frame on its GPU.
 
     ``render()`` runs this rank's rows, gathers to rank 0 and (on rank 0)
-    de-interleaves the frame; everything is asynchronous on the current
+    de-interleaves the frame; everything is asynchronous on the frame's
     stream.  ``fmt`` is "rgba8" (the displayed RenderTexture format; 3 B/px on
     the wire, ``wire="rgb8"``, or 4 with ``wire="rgba8"``) or "float4" (full
     gl_FragColor, 16 B/px, used by parity tests).
 
-    Overlap of the gather (RCCL, xGMI) with rendering, two ways:
+    Overlap, three ways:
     * ``submit()`` / ``flush()`` pipeline consecutive frames: frame k's gather
       runs on RCCL's stream while frame k+1 renders (the wire buffers are
       double-buffered); rank 0 de-interleaves frame k after frame k+1's render
       was enqueued.  One render launch per frame per rank.
+    * ``streams=2`` puts consecutive frames on two HIP streams, so frame k+1's
+      waves fill the SIMDs while frame k's longest waves finish.  A frame's
+      time is bounded below by its slowest pixel (a grazing soft-shadow march
+      of several hundred dependent steps); with 1/8 of a 4096^2 frame per rank
+      that tail is as long as the rest of the frame, and overlapping frames
+      hides it (tools/shard_probe.py: 0.23 -> 0.12 ms per rank at N = 8).
+      Every buffer a frame writes (band, wire, gathered, frame) is per slot.
+      Default: 2 streams when N > 1 and the gather is pipelined (RCCL), else 1.
     * ``chunks`` > 1 pipelines within a frame: the packed rows are cut into
       that many ranges (same cuts on every rank) and chunk k+1 renders while
       chunk k is gathered; it costs a launch tail per chunk.
     """
 
-    def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None, chunks=1, wire="auto"):
+    def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None, chunks=1, wire="auto",
+                 streams=None):
         import torch
 
         self.r, self.rank, self.world, self.fmt, self.group = renderer, rank, world, fmt, group
@@ -112,32 +121,39 @@ class DistributedFrame:
         # one shard: the packed rows are the frame rows (no de-interleave needed)
         self.plan = ShardPlan(W, H, band if world > 1 else H, world)
         dev = torch.device(f"cuda:{renderer.device}")
+        if streams is None:
+            streams = 2 if self._pipelined() else 1
+        if streams not in (1, 2):
+            raise ValueError("streams must be 1 or 2")
+        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(streams - 1)]
         rps = self.plan.rows_per_shard
         self.nmine = self.plan.count(rank)
         chunks = max(1, min(int(chunks), rps))
         self.cuts = [round(c * rps / chunks) for c in range(chunks + 1)]
-        nbuf = 2 if world > 1 else 1
+        nbuf = 2 if world > 1 or streams > 1 else 1
         shape = (rps, W) if fmt == "rgba8" else (rps, W, 4)
         dtype = torch.int32 if fmt == "rgba8" else torch.float32
         if self.wire == "rgb8":
             # render into a local RGBA8 band, pack each chunk into the slot being gathered
-            self.local = torch.empty(shape, dtype=dtype, device=dev)
+            self.locals = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nbuf)]
             self.wires = [torch.empty((rps, 3 * W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
         else:
             # the render kernel writes straight into the slot being gathered
-            self.local = None
+            self.locals = None
             self.wires = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nbuf)]
         wire = self.wires[0]
         self.gathered = ([torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev) for _ in range(2)]
                          if rank == 0 and world > 1 else None)
         if world == 1:
-            self.frame = wire if self.local is None else self.local
+            self.frames = self.wires if self.locals is None else self.locals
         elif rank == 0:
-            self.frame = torch.empty((H, W) if fmt == "rgba8" else (H, W, 4), dtype=dtype, device=dev)
+            self.frames = [torch.empty((H, W) if fmt == "rgba8" else (H, W, 4), dtype=dtype, device=dev)
+                           for _ in range(2)]
         else:
-            self.frame = None
+            self.frames = None
+        self.frame = self.frames[0] if self.frames is not None else None
         self.k = 0            # frames submitted
-        self.pending = None   # (slot, [works]) of the frame whose gather is in flight
+        self.pending = None   # (slot, stream, [works]) of the frame whose gather is in flight
 
     def _pipelined(self):
         import torch.distributed as dist
@@ -148,14 +164,14 @@ class DistributedFrame:
         j1 = min(j1, self.nmine)
         if j1 <= j0:
             return
-        dst = self.wires[slot] if self.local is None else self.local
+        dst = self.wires[slot] if self.locals is None else self.locals[slot]
         if events is not None:
             events[0].record()
         self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, dst[j0:j1])
         if events is not None:
             events[1].record()
-        if self.local is not None:
-            self.r.pack_rgb8(self.local[j0:j1], out=self.wires[slot][j0:j1])
+        if self.locals is not None:
+            self.r.pack_rgb8(self.locals[slot][j0:j1], out=self.wires[slot][j0:j1])
 
     def _gather_async(self, slot, j0, j1):
         import torch.distributed as dist
@@ -165,12 +181,13 @@ class DistributedFrame:
 
     def _deinterleave(self, slot):
         p = self.plan
-        self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered[slot], out=self.frame)
+        self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered[slot],
+                            out=self.frames[slot])
 
     def render_local(self, stats=False):
-        """This rank's rows only, into wire slot 0 (no gather); stats: one synchronous launch."""
+        """This rank's rows only, into slot 0 (no gather); stats: one synchronous launch."""
         p = self.plan
-        dst = self.wires[0] if self.local is None else self.local
+        dst = self.wires[0] if self.locals is None else self.locals[0]
         return self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, 0, self.nmine, dst[: self.nmine],
                                   stats=stats)
 
@@ -178,35 +195,56 @@ class DistributedFrame:
         """Enqueue one frame.  With N > 1 its gather stays in flight until the
         next submit()/flush().  events: optional list of (start, end)
         torch.cuda.Event pairs, one per chunk, recorded around the renders."""
+        import torch
+
         slot = self.k % len(self.wires)
+        st = self.streams[self.k % len(self.streams)]
         self.k += 1
         nch = len(self.cuts) - 1
         works = []
-        for c in range(nch):
-            self._render_rows(self.cuts[c], self.cuts[c + 1], slot, None if events is None else events[c])
-            if self._pipelined():
-                works.append(self._gather_async(slot, self.cuts[c], self.cuts[c + 1]))
-        if self.world > 1 and not self._pipelined():  # gloo: one host-staged gather, completed here
-            gather_to_root(self.wires[slot], self.plan, self.rank, group=self.group,
-                           out=self.gathered[slot] if self.rank == 0 else None)
-            works = None
-        prev, self.pending = self.pending, (slot, works) if self.world > 1 else None
+        with torch.cuda.stream(st):  # the collectives order themselves after this stream
+            self.r.set_stream(st)
+            for c in range(nch):
+                self._render_rows(self.cuts[c], self.cuts[c + 1], slot, None if events is None else events[c])
+                if self._pipelined():
+                    works.append(self._gather_async(slot, self.cuts[c], self.cuts[c + 1]))
+            if self.world > 1 and not self._pipelined():  # gloo: one host-staged gather, completed here
+                gather_to_root(self.wires[slot], self.plan, self.rank, group=self.group,
+                               out=self.gathered[slot] if self.rank == 0 else None)
+                works = None
+        self.r.set_stream(self.streams[0])
+        if self.world == 1:
+            self.frame = self.frames[slot]
+        prev, self.pending = self.pending, (slot, st, works) if self.world > 1 else None
         if prev is not None:
             self._complete(prev)
         return self.frame
 
     def _complete(self, item):
-        slot, works = item
-        for w in works or ():
-            w.wait()
-        if self.rank == 0:
-            self._deinterleave(slot)
+        import torch
+
+        slot, st, works = item
+        with torch.cuda.stream(st):
+            self.r.set_stream(st)
+            for w in works or ():
+                w.wait()  # st waits for the gather
+            if self.rank == 0:
+                self._deinterleave(slot)
+                self.frame = self.frames[slot]
+        self.r.set_stream(self.streams[0])
 
     def flush(self):
-        """Finish the frame in flight (rank 0: its de-interleaved frame is in .frame)."""
+        """Finish the frame in flight (rank 0: its de-interleaved frame is in
+        .frame, ordered before later work on the caller's stream)."""
+        import torch
+
         if self.pending is not None:
             item, self.pending = self.pending, None
             self._complete(item)
+        for st in self.streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            self.streams[0].wait_event(ev)
         return self.frame
 
     def render(self, events=None):

@@ -511,3 +511,90 @@ def test_distributed_frame_two_ranks_on_one_gpu(R, torch_cuda):
     R.set_params(count_evals=0)
     ref = R.render_rgba8(96, 70).cpu().numpy()
     assert np.array_equal(frame, ref)
+
+
+class _FakeWork:
+    def __init__(self, ev=None):
+        self.ev = ev
+
+    def wait(self):
+        import torch
+        if self.ev is not None:
+            torch.cuda.current_stream().wait_event(self.ev)
+
+
+def test_pipelined_two_stream_frames_in_one_process(R, torch_cuda):
+    """DistributedFrame's RCCL path (pipelined gathers, two HIP streams, per-slot
+    buffers) for two ranks living in one process, with the gather replaced by
+    device copies on a side stream that honour the same stream semantics as
+    ProcessGroupNCCL (wait on the caller's stream, work.wait() makes the
+    caller's stream wait).  Every frame of a pose sequence must equal the
+    one-rank rm_render_rgba8 frame."""
+    torch = torch_cuda
+    from raymarching_amd.frame import DistributedFrame
+    W, H, band = 96, 70, 8
+    side = torch.cuda.Stream()
+    sent = {}
+
+    def fake_gather(fr):
+        def gather(slot, j0, j1):
+            ev = torch.cuda.Event()
+            ev.record()  # the caller's (frame) stream
+            if fr.rank == 1:
+                sent[(fr.k, j0)] = (fr.wires[slot][j0:j1], ev)
+                return _FakeWork()
+            src1, ev1 = sent.pop((fr.k, j0))
+            side.wait_event(ev)
+            side.wait_event(ev1)
+            with torch.cuda.stream(side):
+                fr.gathered[slot][0, j0:j1].copy_(fr.wires[slot][j0:j1])
+                fr.gathered[slot][1, j0:j1].copy_(src1)
+            done = torch.cuda.Event()
+            done.record(side)
+            return _FakeWork(done)
+        return gather
+
+    r1 = rm.Renderer(0)
+    frs = []
+    for rank, rr in ((0, R), (1, r1)):
+        f = DistributedFrame.__new__(DistributedFrame)
+        f._pipelined = lambda: True  # as with the "nccl" backend
+        DistributedFrame.__init__(f, rr, W, H, band, rank, 2, fmt="rgba8", chunks=2)
+        f._gather_async = fake_gather(f)
+        frs.append(f)
+    assert len(frs[0].streams) == 2 and frs[0].wire == "rgb8"
+    poses = ["P0", "P1", "P2", "P3"]
+    refs = []
+    for name in poses:
+        setup(R, "T", POSES[name], 128)
+        R.set_params(count_evals=0)
+        refs.append(R.render_rgba8(W, H).cpu().numpy())
+    got = []
+    for i, name in enumerate(poses):
+        for f, rr in ((frs[1], r1), (frs[0], R)):
+            setup(rr, "T", POSES[name], 128)
+            rr.set_params(count_evals=0)
+            f.submit()
+        if i > 0:  # frame i-1 is complete on rank 0 once frame i was submitted
+            torch.cuda.synchronize()
+            got.append(frs[0].frame.cpu().numpy())
+    frs[1].flush()
+    got.append(frs[0].flush().cpu().numpy())
+    torch.cuda.synchronize()
+    for g, ref in zip(got, refs):
+        assert np.array_equal(g, ref)
+    r1.close()
+
+
+def test_single_rank_two_streams(R, torch_cuda):
+    torch = torch_cuda
+    from raymarching_amd.frame import DistributedFrame
+    setup(R, "T", POSES["P4"], 128)
+    R.set_params(count_evals=0)
+    ref = R.render_rgba8(80, 48)
+    fr = DistributedFrame(R, 80, 48, 16, 0, 1, fmt="rgba8", streams=2)
+    for _ in range(3):
+        fr.submit()
+    frame = fr.flush()
+    torch.cuda.synchronize()
+    assert torch.equal(frame, ref)
