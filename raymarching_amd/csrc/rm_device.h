@@ -406,8 +406,12 @@ __device__ __forceinline__ float gpow(float x, float y) {
 template <bool FAST>
 __device__ __forceinline__ float tonemap1(float c, float e2) {
     float col = c * 2.0f / (1.0f + c);
-    col = gpow<FAST>(col, 0.4545f);
-    col = gpow<FAST>(col, e2);
+    if constexpr (FAST) {  // pow(pow(x, .4545), e2) = exp2(.4545 e2 log2 x): one log2, one exp2
+        col = __builtin_amdgcn_exp2f((0.4545f * e2) * __builtin_amdgcn_logf(col));
+    } else {
+        col = gpow<FAST>(col, 0.4545f);
+        col = gpow<FAST>(col, e2);
+    }
     return col * 0.5f + 0.5f * col * col * (3.0f - 2.0f * col);
 }
 // tonemap -> contrast (common.frag:1067) -> vignette(.., 0.1) (:1072)

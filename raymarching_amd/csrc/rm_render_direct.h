@@ -196,6 +196,10 @@ __device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 p, V3 eye, V
 
 template <int SC>
 __device__ __forceinline__ V3 shadow_pow(float sha) {
+    if constexpr (FastMath<SC>::value) {  // pow(x, 1) = x; one log2 shared by the other two
+        const float l = __builtin_amdgcn_logf(sha);
+        return v3(sha, __builtin_amdgcn_exp2f(1.2f * l), __builtin_amdgcn_exp2f(1.5f * l));
+    }
     return v3(mpow<SC>(sha, 1.0f), mpow<SC>(sha, 1.2f), mpow<SC>(sha, 1.5f));
 }
 
