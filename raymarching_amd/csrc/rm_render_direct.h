@@ -211,7 +211,11 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
     for (int i = 0; i < 32; i++) {
         float fi = (float)i;
         float sl = F.hash11[i];
-        V3 rnd = normalize(hash33(nn + v3s(fi)) - v3s(0.5f));
+        // the sample direction is not amplified (unlike the hash of the normal),
+        // so it is normalized with v_rsq (~1 ulp) instead of a correctly
+        // rounded sqrt and division: -22 VALU per sample, 32 samples
+        const V3 hd = hash33(nn + v3s(fi)) - v3s(0.5f);
+        V3 rnd = hd * __builtin_amdgcn_rsqf(dot(hd, hd));
         V3 dir = rnd - (nn * 2.0f) * fminf(0.0f, dot(rnd, nn));  // reflectVector (:70-73)
         th += sl + dist_probe<SC>(F, pos + dir * sl, cnt);
     }
