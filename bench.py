@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--spinup", type=float, default=0.3,
+                    help="seconds of untimed frames before the warm-up frames (GPU clock ramp)")
     ap.add_argument("--scene", default="T")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--height", type=int, default=None)
@@ -206,6 +208,15 @@ def main():
         dist.all_reduce(ev_total)
     evals_rank, evals_frame = int(ev_rank.item()), int(ev_total.item())
 
+    # untimed spin-up before the W warm-up frames: a fresh GPU ramps its clocks
+    # over the first ~0.1 s of load (3 warm-up frames are ~3 ms), so the timed
+    # frames would otherwise include the ramp.  Same frames, same work.
+    t_spin = time.perf_counter()
+    while time.perf_counter() - t_spin < args.spinup:
+        for _ in range(8):
+            fr.submit()
+        fr.flush()
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         fr.submit()
     fr.flush()
