@@ -211,12 +211,19 @@ def main():
     # untimed spin-up before the W warm-up frames: a fresh GPU ramps its clocks
     # over the first ~0.1 s of load (3 warm-up frames are ~3 ms), so the timed
     # frames would otherwise include the ramp.  Same frames, same work.
+    # Every rank runs the same number of rounds (each frame holds a gather), so
+    # whether to go on is agreed over all ranks after each round.
     t_spin = time.perf_counter()
-    while time.perf_counter() - t_spin < args.spinup:
+    while args.spinup > 0:
         for _ in range(8):
             fr.submit()
         fr.flush()
         torch.cuda.synchronize(dev)
+        go = torch.tensor([1.0 if time.perf_counter() - t_spin < args.spinup else 0.0], device=red_dev)
+        if world > 1:
+            dist.all_reduce(go, op=dist.ReduceOp.MIN)
+        if go.item() == 0.0:
+            break
     for _ in range(args.warmup):
         fr.submit()
     fr.flush()
