@@ -158,7 +158,8 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int
     F.mouse_x = c->mouse[0];
     F.mouse_y = c->mouse[1];
     F.max_steps = c->params.max_steps;
-    F.shadow_max_steps = c->params.shadow_max_steps;
+    // 0 (unbounded, the reference) travels as INT_MAX: one compare per shadow step
+    F.shadow_max_steps = c->params.shadow_max_steps > 0 ? c->params.shadow_max_steps : 0x7fffffff;
     for (int i = 0; i < 32; i++) F.hash11[i] = hash11((float)i);
     return F;
 }

@@ -47,7 +47,7 @@ struct FrameConst {
     int nrows;                     // packed rows rendered by this launch
     int row0;                      // first packed row of the shard this launch renders
     int max_steps;                 // MAX_MARCHING_STEPS (common.frag:15), run-time
-    int shadow_max_steps;          // 0 = unbounded, as softshadow2 (common.frag:814)
+    int shadow_max_steps;          // step cap; unbounded (INT_MAX), as softshadow2 (common.frag:814), unless set
     float time;                    // u_time
     float mouse_x, mouse_y;        // u_mouse
     float hash11[32];              // Hash11(i), i = 0..31 (output_shader.frag:54-59,102)

@@ -113,7 +113,7 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
         den = upd ? cd : den;
         P = h + h;
         t = fmaf(h, 0.1f, t + 0.001f);
-        if ((h < 0.001f) | !(t < maxt) | (F.shadow_max_steps > 0 & it >= F.shadow_max_steps)) break;
+        if ((h < 0.001f) | !(t < maxt) | (it >= F.shadow_max_steps)) break;
     }
     return h < 0.001f ? 0.0f : sqrtf(16.0f * num / den);
 }
@@ -145,7 +145,7 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
         den = upd ? cd : den;
         P = h + h;
         t = fmaf(h, 0.1f, t + 0.001f);
-        if ((h < 0.001f) | !(t < maxt) | (F.shadow_max_steps > 0 & it >= F.shadow_max_steps)) break;
+        if ((h < 0.001f) | !(t < maxt) | (it >= F.shadow_max_steps)) break;
     }
     return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(16.0f * num * __builtin_amdgcn_rcpf(den));
 }
