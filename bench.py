@@ -63,6 +63,19 @@ def parse():
     return ap.parse_args()
 
 
+def _config_id(scene, W, H, max_steps, world):
+    """SURVEY.md 8(d) config name for a workload; "custom" when it matches none."""
+    if scene == "S0" and (W, H) == (256, 256):
+        return "C1"
+    if scene == "T" and (W, H, max_steps) == (1920, 1080, 128):
+        return "C2"
+    if scene == "T" and (W, H, max_steps) == (4096, 4096, 256):
+        return "C3" if world == 1 else "C4"
+    if scene == "O" and (W, H, max_steps) == (8192, 8192, 512):
+        return "C5"
+    return "custom"
+
+
 def cpu_baseline(args, pose, W, H, target_s):
     """Oracle (CPU restatement, -O3 build) on a strided row sample of the same frame."""
     import oracle  # test infrastructure: only the cpu_baseline leg uses it
@@ -299,7 +312,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic: uniforms only (camera pose), no input data",
             "config": {
-                "workload": f"C{3 if world == 1 else 4}: {W}x{H} scene {args.scene} "
+                "workload": f"{_config_id(args.scene, W, H, args.max_steps, world)}: {W}x{H} scene {args.scene} "
                             f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
                             f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0",
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
