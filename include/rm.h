@@ -119,6 +119,12 @@ rm_status rm_synchronize(rm_ctx *ctx);
  * buffer and copied back before returning. */
 rm_status rm_render(rm_ctx *ctx, int W, int H, float *out, rm_stats *stats);
 
+/* rm_render through the instrumented kernel, which also writes the number of
+ * sceneSDF calls (ray-steps) each pixel made into evals_map (W*H uint32, row 0
+ * first; the same count as rm_stats.evals, per pixel).  Device or host
+ * buffers.  The parity tests compare it with the reference GLSL's counts. */
+rm_status rm_render_step_map(rm_ctx *ctx, int W, int H, float *out, uint32_t *evals_map, rm_stats *stats);
+
 /* Same pass over one shard of a W x H frame: frame row y belongs to shard
  * (y / band) % nshards; the shard's rows are packed into `out` in increasing
  * y (rm_shard_rows() rows of W float4).  Used by row-sharded multi-GPU frames. */

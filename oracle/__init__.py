@@ -83,6 +83,9 @@ def lib(fast: bool = False) -> ctypes.CDLL:
         L.oracle_bloom_levels.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.oracle_bloom_levels.restype = ctypes.c_int
+        L.oracle_render_diag.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, f32p, f32p]
+        L.oracle_render_diag.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         L.oracle_num_threads.restype = ctypes.c_int
         _LIBS[name] = L
@@ -125,6 +128,22 @@ def render_rows(scene: str, W: int, H: int, rows, fast=False, **kw):
     if rc:
         raise ValueError(f"oracle_render_rows failed rc={rc}")
     return out, ev
+
+
+N_DIAG = 7
+
+
+def render_diag(scene: str, W: int, H: int, **kw):
+    """Scene-O diagnostic channels (make_goldens.py diag_edit) -> (diag f32
+    [H, W, N_DIAG, 4], rgba f32 [H, W, 4])."""
+    u = uniforms(W, H, **kw)
+    diag = np.zeros((H, W, N_DIAG, 4), np.float32)
+    out = np.zeros((H, W, 4), np.float32)
+    rc = lib().oracle_render_diag(SCENES[scene], ctypes.byref(u), W, H, 0, H, _p(diag, ctypes.c_float),
+                                  _p(out, ctypes.c_float))
+    if rc:
+        raise ValueError(f"oracle_render_diag failed rc={rc}")
+    return diag, out
 
 
 def scene_dist(scene: str, pts, **kw):

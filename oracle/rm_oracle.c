@@ -73,7 +73,19 @@ typedef struct {
     float ry_c, ry_s, rx_c, rx_s, rz_c, rz_s;
     uint64_t *evals; /* per-thread counter of sceneSDF calls */
     struct SegRec *rec; /* optional: per-pixel phase/segment recorder (analysis) */
+    float *diag;        /* optional: scene-O diagnostic channels, N_DIAG vec4 per pixel */
+    int lvl;            /* 0 = primary light(), 1 = inside the reflection bounce */
 } Ctx;
+
+/* Diagnostic channels of make_goldens.py diag_edit (test aid, values only):
+ * 0 primary normal, dist; 1 primary thickness, sha, occ, ind; 2 primary light()
+ * colour, fresnel; 3 reflection normal, dist (-1 miss); 4 reflection thickness,
+ * sha, occ, ind; 5 reflection colour; 6 render() colour.  Unset = -9. */
+#define N_DIAG 7
+static inline void diag_set(const Ctx *C, int k, float a, float b, float c, float d) {
+    if (!C->diag) return;
+    C->diag[4 * k] = a; C->diag[4 * k + 1] = b; C->diag[4 * k + 2] = c; C->diag[4 * k + 3] = d;
+}
 
 /* Analysis aid (not part of the restatement): records, per pixel, the
  * sequence of sceneSDF-call segments as (phase, count) pairs, so the SIMD
@@ -110,7 +122,10 @@ static inline vec3 divs(vec3 a, float s) { return v3(a.x / s, a.y / s, a.z / s);
 static inline vec3 neg(vec3 a) { return v3(-a.x, -a.y, -a.z); }
 static inline float dot3(vec3 a, vec3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static inline float length3(vec3 a) { return sqrtf(dot3(a, a)); }
-static inline vec3 normalize3(vec3 a) { return divs(a, length3(a)); }
+/* GLSL normalize(x) = x / length(x); the pinned implementation (SwiftShader,
+ * tests/golden) multiplies by the correctly rounded reciprocal of the length
+ * (bit-exact on 8192 vectors, tools/ss_probe.py) */
+static inline vec3 normalize3(vec3 a) { return muls(a, 1.0f / length3(a)); }
 /* GLSL 1.30 spec 8.3: min(x,y) = y < x ? y : x ; max(x,y) = x < y ? y : x */
 static inline float gmin(float x, float y) { return y < x ? y : x; }
 static inline float gmax(float x, float y) { return x < y ? y : x; }
@@ -135,6 +150,29 @@ static inline vec3 refract3(vec3 I, vec3 N, float eta) {
     return sub(muls(I, eta), muls(N, eta * d + sqrtf(k)));
 }
 static inline float radians(float deg) { return deg * 0.017453292519943295f; }
+
+/* GLSL sin()/cos().  GLSL leaves their precision to the implementation
+ * (parity unpinned at that level); these restate the implementation that
+ * renders the golden fixtures (SwiftShader 4.1, tests/golden/make_goldens.py):
+ * reduce to y = x/2pi - round(y) in [-1/2, 1/2], evaluate the cos/sin of
+ * pi*y by two minimax polynomials, double the angle twice and normalize
+ * ("A Fast, Vectorizable Algorithm for Producing Single-Precision Sine-Cosine
+ * Pairs"); cos(x) = sin(x + 1.57079632).  Bit-exact against SwiftShader on
+ * 8000 arguments in [-400, 400] (tools/ss_probe.py).  The uniform-derived
+ * rotations (camera rot(), transformR) and floorMat use them: a ulp of the
+ * sponge rotation moves the sampled distances that getNormalFast
+ * differentiates, and the normal feeds the Hash33 of CalculateThickness. */
+static float glsl_sin(float x) {
+    float y = x * 1.59154943e-1f;
+    y = y - rintf(y);
+    float y2 = y * y;
+    float c1 = y2 * (y2 * (y2 * -0.0204391631f + 0.2536086171f) + -1.2336977925f) + 1.0f;
+    float s1 = y * (y2 * (y2 * (y2 * -0.0046075748f + 0.0796819754f) + -0.645963615f) + 1.5707963235f);
+    float c2 = c1 * c1 - s1 * s1;
+    float s2 = 2.0f * s1 * c1;
+    return 2.0f * s2 * c2 * (1.0f / (s2 * s2 + c2 * c2));
+}
+static float glsl_cos(float x) { return glsl_sin(x + 1.57079632f); }
 
 /* ------------------------------------------------------------- constants */
 
@@ -540,6 +578,7 @@ static vec3 light(const Ctx *C, const Material *mat, vec3 ro, vec3 rd, vec3 p, v
     float SSSPower = 1.1f;
     float SSSScale = 0.3f;
     float thickness = CalculateThickness(C, p, n);
+    diag_set(C, C->lvl == 0 ? 1 : 4, thickness, sha, occ, ind);
     vec3 toEye = neg(rd);
     vec3 SSSLight = add(lightDir, muls(n, SSSDistortion));
     float SSSDot = powf(gclamp(dot3(toEye, neg(SSSLight)), 0.0f, 1.0f), SSSPower) * SSSScale;
@@ -571,9 +610,15 @@ static vec3 renderReflection(const Ctx *C, vec3 ro, vec3 rd) {
     if (sd.dist > 0.0f) {
         vec3 p = add(ro, muls(rd, sd.dist));
         vec3 n = getNormalFast(C, p);
-        return light(C, &sd.mat, ro, rd, p, n, n);
+        diag_set(C, 3, n.x, n.y, n.z, sd.dist);
+        vec3 lc = light(C, &sd.mat, ro, rd, p, n, n);
+        diag_set(C, 5, lc.x, lc.y, lc.z, 0.0f);
+        return lc;
     }
-    return background(ro, rd);
+    diag_set(C, 3, 0.0f, 0.0f, 0.0f, -1.0f);
+    vec3 bc = background(ro, rd);
+    diag_set(C, 5, bc.x, bc.y, bc.z, 0.0f);
+    return bc;
 }
 
 /* output_shader.frag:298-343 (MAX_REFRACTIONS 4) */
@@ -614,10 +659,13 @@ static vec3 render_O(const Ctx *C, vec3 ro, vec3 rd) {
     if (sd.dist > 0.0f) {
         vec3 p = add(ro, muls(rd, sd.dist));
         vec3 n = getNormalFast(C, p);
+        diag_set(C, 0, n.x, n.y, n.z, sd.dist);
         vec3 color = light(C, &sd.mat, ro, rd, p, n, n);
         float reflect_factor = fresnelReflection(sd.mat.refraction_index, n, rd,
                                                  sd.mat.transparency > 0.0f ? 0.0f : sd.mat.reflectivity);
         float refract_factor = 1.0f - reflect_factor;
+        diag_set(C, 2, color.x, color.y, color.z, reflect_factor);
+        ((Ctx *)C)->lvl = 1;
         if (sd.mat.reflectivity > 0.0f) {
             vec3 reflected_rd = reflect3(rd, n);
             vec3 rc = renderReflection(C, add(p, muls(reflected_rd, 0.001f)), reflected_rd);
@@ -628,6 +676,7 @@ static vec3 render_O(const Ctx *C, vec3 ro, vec3 rd) {
             vec3 rc = renderRefraction(C, add(p, muls(refracted_rd, 0.001f)), refracted_rd, sd.mat.absorption);
             color = add(color, muls(muls(rc, refract_factor), sd.mat.transparency));
         }
+        diag_set(C, 6, color.x, color.y, color.z, 0.0f);
         return color;
     }
     return background(ro, rd);
@@ -685,12 +734,12 @@ static void shade_pixel(const Ctx *C, int W, int H, int col, int row, float *out
     vec3 rd = normalize3(v3(uv.x, -uv.y, -1.0f));
     /* rd.yz *= rot(-u_mouse.y); rd.xz *= rot(u_mouse.x)   (common.frag:1088-1092) */
     float a = -C->u.mouse_y;
-    float s = sinf(a), c = cosf(a);
+    float s = glsl_sin(a), c = glsl_cos(a);
     float y = rd.y * c + rd.z * -s;
     float z = rd.y * s + rd.z * c;
     rd.y = y; rd.z = z;
     a = C->u.mouse_x;
-    s = sinf(a); c = cosf(a);
+    s = glsl_sin(a); c = glsl_cos(a);
     float x = rd.x * c + rd.z * -s;
     z = rd.x * s + rd.z * c;
     rd.x = x; rd.z = z;
@@ -714,9 +763,9 @@ static void init_ctx(Ctx *C, int scene, const oracle_uniforms *u) {
      * template.frag:41): rotationY(-rot.y), rotationX(-rot.x), rotationZ(-rot.z) */
     float rot_x = 180.0f, rot_y = u->time * 2.0f, rot_z = 0.0f;
     float ay = radians(-rot_y), ax = radians(-rot_x), az = radians(-rot_z);
-    C->ry_c = cosf(ay); C->ry_s = sinf(ay);
-    C->rx_c = cosf(ax); C->rx_s = sinf(ax);
-    C->rz_c = cosf(az); C->rz_s = sinf(az);
+    C->ry_c = glsl_cos(ay); C->ry_s = glsl_sin(ay);
+    C->rx_c = glsl_cos(ax); C->rx_s = glsl_sin(ax);
+    C->rz_c = glsl_cos(az); C->rz_s = glsl_sin(az);
 }
 
 /* ---------------------------------------------------------- exported API */
@@ -786,6 +835,30 @@ int oracle_render_segments(int scene, const oracle_uniforms *u, int W, int H, in
             memset(rec.out, 0, MAX_SEG * 2 * sizeof(uint16_t));
             shade_pixel(&C, W, H, x, row0 + r, px);
             nseg[i] = (uint8_t)rec.nseg;
+        }
+    }
+    return 0;
+}
+
+/* Scene-O diagnostic channels (N_DIAG vec4 per pixel, -9 = unset) of rows
+ * [row0, row0+nrows), plus the image (out, may be NULL) -- test aid. */
+int oracle_render_diag(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, float *diag,
+                       float *out) {
+    if (!u || !diag || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H) return 1;
+    if (scene != SCENE_O && scene != SCENE_OG) return 2;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; r++) {
+        Ctx C;
+        uint64_t cnt = 0;
+        float px[4];
+        init_ctx(&C, scene, u);
+        C.evals = &cnt;
+        for (int x = 0; x < W; x++) {
+            size_t i = (size_t)r * W + x;
+            C.diag = diag + i * 4 * N_DIAG;
+            C.lvl = 0;
+            for (int k = 0; k < 4 * N_DIAG; k++) C.diag[k] = -9.0f;
+            shade_pixel(&C, W, H, x, row0 + r, out ? out + i * 4 : px);
         }
     }
     return 0;

@@ -23,7 +23,7 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8",
            "rm_pack_rgba8", "rm_pack_rgb8", "rm_deinterleave_rgb8",
            "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_last_error", "rm_status_string",
-           "rm_compile_scene", "rm_scene_eval")
+           "rm_compile_scene", "rm_scene_eval", "rm_render_step_map")
 
 
 class RmParams(ctypes.Structure):
@@ -78,6 +78,7 @@ def lib() -> ctypes.CDLL:
         "rm_set_stream": ([vp, vp], c.c_int),
         "rm_synchronize": ([vp], c.c_int),
         "rm_render": ([vp, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
+        "rm_render_step_map": ([vp, c.c_int, c.c_int, vp, vp, c.POINTER(RmStats)], c.c_int),
         "rm_render_band": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
         "rm_render_rows": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp,
                             c.POINTER(RmStats)], c.c_int),

@@ -116,6 +116,22 @@ class Renderer:
               self._ctx)
         return (out, s.as_dict()) if stats else out
 
+    def render_step_map(self, W: int, H: int, out=None, evals_map=None):
+        """Full frame plus the per-pixel sceneSDF call counts: (float32 [H, W, 4],
+        int32 [H, W], stats), device tensors (allocated if None)."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        if out is None:
+            out = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+        if evals_map is None:
+            evals_map = torch.empty((H, W), dtype=torch.int32, device=dev)
+        _check_out(out, H * W * 4)
+        _check_out(evals_map, H * W)
+        s = RmStats()
+        check(lib().rm_render_step_map(self._ctx, int(W), int(H), self._ptr(out), self._ptr(evals_map),
+                                       ctypes.byref(s)), self._ctx)
+        return out, evals_map, s.as_dict()
+
     def render_band(self, W: int, H: int, band: int, nshards: int, shard: int, out=None, stats: bool = False):
         """Rows y with (y // band) % nshards == shard, packed in increasing y."""
         torch = _torch()

@@ -144,14 +144,14 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int
     F.pos_x = c->pos[0]; F.pos_y = c->pos[1]; F.pos_z = c->pos[2];
     // rot(a) = mat2(cos a, -sin a, sin a, cos a) (common.frag:1088-1092)
     float a1 = -c->mouse[1], a2 = c->mouse[0];
-    F.cam1_c = std::cos(a1); F.cam1_s = std::sin(a1);
-    F.cam2_c = std::cos(a2); F.cam2_s = std::sin(a2);
+    F.cam1_c = rm::glsl_cos(a1); F.cam1_s = rm::glsl_sin(a1);
+    F.cam2_c = rm::glsl_cos(a2); F.cam2_s = rm::glsl_sin(a2);
     // transformR(.., vec3(180, u_time * 2, 0)): rotationY(-rot.y), rotationX(-rot.x)
     // with radians(x) = x * pi/180 (common.frag:190-214,434-441)
     float rot_y = c->time * 2.0f, rot_x = 180.0f;
     float ay = -rot_y * 0.017453292519943295f, ax = -rot_x * 0.017453292519943295f;
-    F.ry_c = std::cos(ay); F.ry_s = std::sin(ay);
-    F.rx_c = std::cos(ax); F.rx_s = std::sin(ax);
+    F.ry_c = rm::glsl_cos(ay); F.ry_s = rm::glsl_sin(ay);
+    F.rx_c = rm::glsl_cos(ax); F.rx_s = rm::glsl_sin(ax);
     F.W = W; F.H = H;
     F.band = band; F.nshards = nshards; F.shard = shard; F.nrows = nrows;
     F.time = c->time;
@@ -192,10 +192,11 @@ int pick_kernel(const rm_ctx *c) {
 // the pass over packed rows [row0, row0 + count) of a shard: device output,
 // optional stats (synchronous when given)
 rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, void *out,
-                     bool rgba8, rm_stats *stats) {
+                     bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr) {
     FrameConst F = frame_const(ctx, W, H, band, nshards, shard, count);
     F.row0 = row0;
-    bool cnt = ctx->params.count_evals != 0;
+    F.evals_map = evmap;
+    bool cnt = ctx->params.count_evals != 0 || evmap;
     if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 2 * sizeof(unsigned long long), ctx->stream));
     if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     hipError_t e =
@@ -221,7 +222,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
 
 // row_count < 0: every packed row from row_begin on; out: float4 or RGBA8 rows
 rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
-                     void *out, bool rgba8, rm_stats *stats) {
+                     void *out, bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
@@ -239,13 +240,20 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     }
     if (!out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: null output");
     RM_HIP(hipSetDevice(ctx->device));
-    if (is_device_ptr(out)) return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, out, rgba8, stats);
-    size_t bytes = (size_t)W * row_count * (rgba8 ? sizeof(uint32_t) : sizeof(float4));
-    rm_status s = ensure_staging(ctx, bytes);
+    const bool dev_out = is_device_ptr(out), dev_map = !evmap || is_device_ptr(evmap);
+    if (dev_out && dev_map)
+        return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, out, rgba8, stats, evmap);
+    // host buffers go through the staging buffer: the frame, then the step map
+    const size_t bytes = dev_out ? 0 : (size_t)W * row_count * (rgba8 ? sizeof(uint32_t) : sizeof(float4));
+    const size_t map_bytes = dev_map ? 0 : (size_t)W * row_count * sizeof(uint32_t);
+    rm_status s = ensure_staging(ctx, bytes + map_bytes);
     if (s != RM_OK) return s;
-    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, ctx->staging, rgba8, stats);
+    char *st = reinterpret_cast<char *>(ctx->staging);
+    uint32_t *map_d = dev_map ? evmap : reinterpret_cast<uint32_t *>(st + bytes);
+    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, dev_out ? out : st, rgba8, stats, map_d);
     if (s != RM_OK) return s;
-    RM_HIP(hipMemcpyAsync(out, ctx->staging, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (!dev_out) RM_HIP(hipMemcpyAsync(out, st, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (!dev_map) RM_HIP(hipMemcpyAsync(evmap, map_d, map_bytes, hipMemcpyDeviceToHost, ctx->stream));
     RM_HIP(hipStreamSynchronize(ctx->stream));
     return RM_OK;
 }
@@ -385,6 +393,11 @@ rm_status rm_synchronize(rm_ctx *ctx) {
 
 rm_status rm_render(rm_ctx *ctx, int W, int H, float *out, rm_stats *stats) {
     return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, out, false, stats);
+}
+
+rm_status rm_render_step_map(rm_ctx *ctx, int W, int H, float *out, uint32_t *evals_map, rm_stats *stats) {
+    if (!evals_map) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_step_map: null evals_map");
+    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, out, false, stats, evals_map);
 }
 
 rm_status rm_render_band(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, float *out, rm_stats *stats) {

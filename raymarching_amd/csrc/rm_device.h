@@ -51,6 +51,7 @@ struct FrameConst {
     float time;                    // u_time
     float mouse_x, mouse_y;        // u_mouse
     float hash11[32];              // Hash11(i), i = 0..31 (output_shader.frag:54-59,102)
+    uint32_t* evals_map;           // instrumented launches: sceneSDF calls per pixel (packed rows), or null
 };
 
 // A scene plugin's sceneSDF, bound in the plugin's translation unit
@@ -100,6 +101,28 @@ __device__ __forceinline__ V3 refract(V3 I, V3 N, float eta) {
     if (k < 0.0f) return v3s(0.0f);
     return I * eta - N * (eta * d + sqrtf(k));
 }
+
+// GLSL sin()/cos().  GLSL leaves their precision to the implementation; these
+// restate the implementation that renders the golden fixtures (SwiftShader
+// 4.1, tests/golden/make_goldens.py): y = x/2pi - round(x/2pi), cos/sin of
+// pi*y by two minimax polynomials, the angle doubled twice and renormalized;
+// cos(x) = sin(x + 1.57079632).  Bit-exact against it on 8000 arguments
+// (tools/ss_probe.py).  Used for the per-frame rotations (camera rot() and
+// transformR, computed on the host) and floorMat: a ulp of the sponge rotation
+// moves the distances getNormalFast differentiates, and the normal feeds the
+// Hash33 of CalculateThickness.  No contraction.
+__host__ __device__ inline float glsl_sin(float x) {
+#pragma clang fp contract(off)
+    float y = x * 1.59154943e-1f;
+    y = y - __builtin_rintf(y);
+    const float y2 = y * y;
+    const float c1 = y2 * (y2 * (y2 * -0.0204391631f + 0.2536086171f) + -1.2336977925f) + 1.0f;
+    const float s1 = y * (y2 * (y2 * (y2 * -0.0046075748f + 0.0796819754f) + -0.645963615f) + 1.5707963235f);
+    const float c2 = c1 * c1 - s1 * s1;
+    const float s2 = 2.0f * s1 * c1;
+    return 2.0f * s2 * c2 * (1.0f / (s2 * s2 + c2 * c2));
+}
+__host__ __device__ inline float glsl_cos(float x) { return glsl_sin(x + 1.57079632f); }
 
 // ------------------------------------------------------------------ SDFs
 
@@ -353,8 +376,8 @@ __device__ __forceinline__ Mat mat_mirror() {  // output_shader.frag:15
 // output_shader.frag:16-28
 __device__ __forceinline__ Mat floor_mat(V3 pos) {
     float scale = fmaxf(10.0f, powf(length(pos), 1.3f));
-    float tx = smoothstep(-0.005f, 0.005f, sinf(pos.x * PI_REF) / scale);
-    float ty = smoothstep(-0.005f, 0.005f, sinf(pos.z * PI_REF) / scale);
+    float tx = smoothstep(-0.005f, 0.005f, glsl_sin(pos.x * PI_REF) / scale);
+    float ty = smoothstep(-0.005f, 0.005f, glsl_sin(pos.z * PI_REF) / scale);
     float tile = fminf(fmaxf(tx, ty), fmaxf(1.0f - tx, 1.0f - ty));
     V3 color = mix3(v3s(0.3f), v3s(0.025f), tile);
     return mat_make(color, v3s(0.03f), 128.0f, 0.0f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));

@@ -37,6 +37,7 @@ extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst
         else static_cast<float4*>(out)[i] = make_float4(c.x, c.y, c.z, 1.0f);
     }
     if (evals) {
+        if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;
         uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop);
         if (lane == 0) {
             atomicAdd(&evals[0], (unsigned long long)se);

@@ -112,7 +112,7 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
         num = upd ? cn : num;
         den = upd ? cd : den;
         P = h + h;
-        t = fmaf(h, 0.1f, t + 0.001f);
+        t += h * 0.1f + 0.001f;  // the reference's roundings: the step count is part of parity
         if ((h < 0.001f) | !(t < maxt) | (it >= F.shadow_max_steps)) break;
     }
     return h < 0.001f ? 0.0f : sqrtf(16.0f * num / den);
@@ -454,6 +454,7 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
         else out[(size_t)j * F.W + x] = make_float4(c.x, c.y, c.z, 1.0f);
     }
     if constexpr (COUNT) {
+        if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;
         uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop);
         if (lane == 0) {
             atomicAdd(&evals[0], (unsigned long long)se);

@@ -125,8 +125,9 @@ __device__ __forceinline__ float log(float x) { return logf(x); }
 __device__ __forceinline__ float log2(float x) { return log2f(x); }
 __device__ __forceinline__ float sqrt(float x) { return sqrtf(x); }
 __device__ __forceinline__ float inversesqrt(float x) { return 1.0f / sqrtf(x); }
-__device__ __forceinline__ float sin(float x) { return sinf(x); }
-__device__ __forceinline__ float cos(float x) { return cosf(x); }
+// sin/cos as the implementation that renders the golden fixtures (rm_device.h glsl_sin)
+__device__ __forceinline__ float sin(float x) { return glsl_sin(x); }
+__device__ __forceinline__ float cos(float x) { return glsl_cos(x); }
 __device__ __forceinline__ float tan(float x) { return tanf(x); }
 __device__ __forceinline__ float asin(float x) { return asinf(x); }
 __device__ __forceinline__ float acos(float x) { return acosf(x); }
@@ -188,7 +189,7 @@ __device__ __forceinline__ float dot(vec2 a, vec2 b) { return a.x * b.x + a.y * 
 __device__ __forceinline__ float dot(vec4 a, vec4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
 __device__ __forceinline__ float length(vec2 a) { return sqrtf(dot(a, a)); }
 __device__ __forceinline__ float distance(vec3 a, vec3 b) { return length(a - b); }
-__device__ __forceinline__ vec2 normalize(vec2 a) { return a / length(a); }
+__device__ __forceinline__ vec2 normalize(vec2 a) { return a * (1.0f / length(a)); }
 // dot, length, normalize, reflect and refract of vec3 are rm_device.h's (found
 // through the argument type)
 __device__ __forceinline__ vec3 cross(vec3 a, vec3 b) {

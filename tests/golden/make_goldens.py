@@ -119,12 +119,20 @@ def count_hook(s: str, sig: str) -> str:
     return s[:k] + "\n\tif (g_cnt_off == 0) g_evals++;" + s[k:]
 
 
+# gl_TexCoord[0].xy of the ray-march pass: the exact pixel-centre coordinate
+# ((x + .5)/W, (y + .5)/H), row 0 first.  A rasterizer interpolates the
+# varying to within an ulp of it (SwiftShader's v_uv is 1 ulp off on 1/3 of
+# the columns of a 96-wide target); the fixtures feed the
+# exact value, which is what the oracle and the HIP path compute.
+EXACT_TC = "((vec2(floor(gl_FragCoord.x), u_resolution.y - 1.0 - floor(gl_FragCoord.y)) + 0.5) / u_resolution)"
+
+
 def main_rewrite(s: str) -> str:
-    s = s.replace("gl_TexCoord[0].xy", "v_uv")
-    head, sep, tail = s.rpartition("col = vignette(col, v_uv);")
+    s = s.replace("gl_TexCoord[0].xy", EXACT_TC)
+    head, sep, tail = s.rpartition(f"col = vignette(col, {EXACT_TC});")
     if not sep:
         raise RuntimeError("vignette call not found")
-    s = head + "col = vignette(col, v_uv, 0.1);" + tail
+    s = head + f"col = vignette(col, {EXACT_TC}, 0.1);" + tail
     # only the live main() (the last one; common.frag:1124-1188 holds commented-out ones)
     head, sep, tail = s.rpartition("gl_FragColor = vec4(col, 1.0);")
     if not sep:
@@ -146,6 +154,79 @@ def scene_O(ref: str, edit=None) -> str:
     s = must_sub("float reflectivity = 0.0)", "float reflectivity)", s)  # output_shader.frag:246
     s = count_hook(s, "SdResult sceneSDF(vec3 p)\n{")
     return HEADER + main_rewrite(s)
+
+
+# Diagnostic channels (DIAG_* fixtures): intermediate values of scene O's
+# render() per pixel, recorded from the reference GLSL so that a parity
+# residual can be attributed term by term.  Seven vec4:
+#   0 primary hit: normal n, castRayD dist      1 primary light(): thickness, sha, occ, ind
+#   2 primary light() colour, fresnel factor     3 reflection hit: normal, dist (-1: miss)
+#   4 reflection light(): thickness, sha, occ, ind
+#   5 reflection colour (light() or background)  6 render() colour (pre-tonemap)
+# Unset channels hold -9.
+N_DIAG = 7
+DIAG_HEADER = "vec4 g_d[7] = vec4[7](vec4(-9.0), vec4(-9.0), vec4(-9.0), vec4(-9.0), vec4(-9.0), vec4(-9.0), vec4(-9.0));\n" \
+              "int g_lvl = 0;\n"
+
+
+def diag_edit(s: str) -> str:
+    """Record the diagnostic channels in output_shader.frag's render()/light()/
+    renderReflection() (reference text; lines output_shader.frag:127-176,
+    246-262, 348-385).  Values only are copied out; no arithmetic changes."""
+    s = must_sub("\t\tvec3 n = getNormalFast(p);\n\t\t\n\t\t// light the surface",
+                 "\t\tvec3 n = getNormalFast(p);\n\t\tg_d[0] = vec4(n, sd.dist);\n\t\t\n\t\t// light the surface", s, count=1)
+    s = must_sub("\t\tvec3 n = getNormalFast(p);\n\t\t\n        return light(sd.mat, ro, rd, p, n);",
+                 "\t\tvec3 n = getNormalFast(p);\n\t\tg_d[3] = vec4(n, sd.dist);\n\t\t\n"
+                 "        vec3 lc_ = light(sd.mat, ro, rd, p, n); g_d[5] = vec4(lc_, 0.0); return lc_;", s, count=1)
+    s = must_sub("\telse // render background (for example: skybox or gradient)\n\t{\n\t\treturn background(ro, rd);\n\t}\t\n}",
+                 "\telse // render background (for example: skybox or gradient)\n\t{\n"
+                 "\t\tg_d[3] = vec4(0.0, 0.0, 0.0, -1.0); vec3 bc_ = background(ro, rd); g_d[5] = vec4(bc_, 0.0); return bc_;\n\t}\t\n}",
+                 s, count=1)
+    s = must_sub("\tfloat thickness = CalculateThickness(p, n);\n",
+                 "\tfloat thickness = CalculateThickness(p, n);\n"
+                 "\tif (g_lvl == 0) g_d[1] = vec4(thickness, sha, occ, ind); else g_d[4] = vec4(thickness, sha, occ, ind);\n", s)
+    s = must_sub("\t\tif (sd.mat.reflectivity > 0)\n\t\t{",
+                 "\t\tg_d[2] = vec4(color, reflect_factor); g_lvl = 1;\n\t\tif (sd.mat.reflectivity > 0)\n\t\t{", s, count=1)
+    s = must_sub("        return color;\n\t}\n\telse // render background",
+                 "        g_d[6] = vec4(color, 0.0); return color;\n\t}\n\telse // render background", s, count=1)
+    return s
+
+
+def scene_O_diag(ref: str) -> str:
+    s = scene_O(ref, diag_edit)
+    s = must_sub("int g_cnt_off = 0;\n", "int g_cnt_off = 0;\n" + DIAG_HEADER, s, count=1)
+    return must_sub("#ifdef COUNT_MODE\n", "#ifdef DIAG_K\n\to_col = g_d[DIAG_K];\n#elif defined(COUNT_MODE)\n", s, count=1)
+
+
+def scene_OG(ref: str) -> str:
+    """output_shader.frag with its blue material made transparent (0.9 in
+    place of 0.0 at output_shader.frag:14): the sphere and the cube then drive
+    renderRefraction (:298-343) and castRayDI (common.frag:903-925), which the
+    reference scene never reaches.  The build's test scene "OG"."""
+    def edit(s):
+        s = must_sub("vec3(0.02, 0.02, 0.04), 32.0, 0.0, 0.0, vec3(2.0, 2.0, 0.75) * 0.2",
+                     "vec3(0.02, 0.02, 0.04), 32.0, 0.0, 0.9, vec3(2.0, 2.0, 0.75) * 0.2", s, count=1)
+        return refraction_loop_flags(s)
+    return scene_O(ref, edit)
+
+
+def refraction_loop_flags(s: str) -> str:
+    """renderRefraction's two `break`s (output_shader.frag:320,332) as a done
+    flag that guards the rest of the body and ends the loop: the same
+    control flow.  SwiftShader (the fixture renderer) executes the straight
+    sceneSDF calls after a `break` of its unrolled loop for the exited lane
+    (getNormalFast and ambientOcclusionReal: +8 counted calls on every
+    refracting pixel, measured); the colours were unaffected.  Fixture
+    bookkeeping only, the arithmetic is untouched."""
+    s = must_sub("\tfor (int i = 0; i < MAX_REFRACTIONS; i++)\n\t{\n\t\tSdResult sd;",
+                 "\tbool done_ = false;\n\tfor (int i = 0; i < MAX_REFRACTIONS && !done_; i++)\n\t{\n\t\tSdResult sd;", s,
+                 count=1)
+    s = must_sub("\t\t\t\tcolor += background(ro, rd);\n\t\t\tbreak;\n\t\t}\n",
+                 "\t\t\t\tcolor += background(ro, rd);\n\t\t\tdone_ = true;\n\t\t}\n\t\tif (!done_) {\n", s, count=1)
+    s = must_sub("\t\tif (invert > 0.0)\n\t\t\tbreak;\n",
+                 "\t\tif (invert > 0.0)\n\t\t\tdone_ = true;\n\t\tif (!done_) {\n", s, count=1)
+    return must_sub("\t\tinvert = tif ? invert : invert * -1.0;\n\t}\n",
+                    "\t\tinvert = tif ? invert : invert * -1.0;\n\t\t}}\n\t}\n", s, count=1)
 
 
 def scene_MB(ref: str) -> str:
@@ -575,6 +656,10 @@ FIXTURES = [
     ("O_96x54_P2", "O", 96, 54, "P2", 128),
     ("O_64_P6", "O", 64, 64, "P6", 128),
     ("O_72x40_P3_512", "O", 72, 40, "P3", 512),
+    # the refraction path (blue made transparent): scene OG
+    ("OG_96x54_P1", "OG", 96, 54, "P1", 128),
+    ("OG_64_P7", "OG", 64, 64, "P7", 128),
+    ("OG_72x40_P3", "OG", 72, 40, "P3", 128),
     # scene plugins (raymarching_amd/scenes/*.hip) against the same reference text
     ("MB_64_P0", "MB", 64, 64, "P0", 128),
     ("MB_72x40_P3", "MB", 72, 40, "P3", 128),
@@ -583,12 +668,22 @@ FIXTURES = [
 ]
 
 
+DIAG_FIXTURES = [
+    # name, W, H, pose, max_steps (scene O)
+    ("DIAG_O_96x54_P2", 96, 54, "P2", 128),
+    ("DIAG_O_64_P6", 64, 64, "P6", 128),
+]
+DIAG_DOC = ["primary normal.xyz, dist", "primary thickness, sha, occ, ind", "primary light colour.rgb, fresnel",
+            "reflection normal.xyz, dist (-1 miss)", "reflection thickness, sha, occ, ind",
+            "reflection colour.rgb", "render colour.rgb (pre-tonemap)"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--only", default=None)
     args = ap.parse_args()
-    builders = {"O": scene_O, "T": scene_T, "S0": scene_S0, "MB": scene_MB, "SC": scene_SC}
+    builders = {"O": scene_O, "OG": scene_OG, "T": scene_T, "S0": scene_S0, "MB": scene_MB, "SC": scene_SC}
     for name, scene, W, H, pose_name, steps in FIXTURES:
         if args.only and args.only not in name:
             continue
@@ -607,6 +702,24 @@ def main():
                             meta=json.dumps(meta))
         print(f"{name}: {dt:.2f}s mean={rgba[..., :3].mean():.4f} evals/px={cnt[..., 0].mean():.2f} "
               f"nan={int(np.isnan(rgba).sum())}")
+    # scene-O diagnostic channels (diag_edit) at the poses of two O fixtures
+    for name, W, H, pose_name, steps in DIAG_FIXTURES:
+        if args.only and args.only not in name:
+            continue
+        pose = POSES[pose_name]
+        src = set_max_steps(scene_O_diag(args.ref), steps)
+        g = GL(W, H)
+        chans = []
+        for k in range(N_DIAG):
+            chans.append(g.draw(g.program(src.replace("precision highp int;\n",
+                                                      f"precision highp int;\n#define DIAG_K {k}\n", 1)), pose, (W, H)))
+        rgba = g.draw(g.program(src), pose, (W, H))
+        meta = dict(scene="O", W=W, H=H, pose=pose_name, pos=list(pose["pos"]), mouse=list(pose["mouse"]),
+                    time=pose["time"], max_steps=steps, renderer=g.renderer, channels=DIAG_DOC,
+                    generator="tests/golden/make_goldens.py (diag_edit)")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), diag=np.stack(chans, axis=2), rgba=rgba,
+                            meta=json.dumps(meta))
+        print(f"{name}: {N_DIAG} channels, primary hits {int(np.sum(chans[0][..., 3] > 0))}")
     # scene-library known answers (lib_kat_cases.py) for the plugin dialect
     if not args.only or args.only in "LIB_kat":
         from lib_kat_cases import CASES, N_POINTS

@@ -26,8 +26,10 @@ def diff_stats(a, b):
 POLICY = {
     "S0": dict(f2e3=0.999, f1e2=1.0, mean=1e-4),
     "T": dict(f2e3=0.99, f1e2=0.995, mean=1e-3),
-    "O": dict(f2e3=0.95, f1e2=0.99, mean=2e-3),
-    "OG": dict(f2e3=0.95, f1e2=0.99, mean=2e-3),
+    # SURVEY.md 8(c)'s policy (99 % within 2e-3, mean <= 1e-3); the residual
+    # of round 1 was attributed and removed
+    "O": dict(f2e3=0.99, f1e2=0.999, mean=1e-3),
+    "OG": dict(f2e3=0.99, f1e2=0.999, mean=1e-3),
     # scene plugins (raymarching_amd/scenes): the mandelbulb's pow/atan/acos
     # orbit is the most ulp-sensitive SDF of the library
     "MB": dict(f2e3=0.9, f1e2=0.97, mean=5e-3),

@@ -15,7 +15,11 @@ from tests.parity import assert_parity, diff_stats
 pytestmark = pytest.mark.gpu
 
 GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
-                if os.path.basename(p).startswith(("S0_", "T_", "O_")))
+                if os.path.basename(p).startswith(("S0_", "T_", "O_", "OG_")))
+
+# per-pixel ray-step maps: fraction of pixels whose sceneSDF call count equals
+# the reference GLSL's (SURVEY.md 8(c) asks >= 95 %)
+STEP_MAP_EXACT = 0.95
 
 
 @pytest.fixture(scope="module")
@@ -53,15 +57,24 @@ def check_evals(st, ev, tol=5e-3):
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
 def test_hip_matches_reference_glsl_golden(R, path):
+    """Image and per-pixel ray-step map against the reference GLSL's.  Pixels
+    whose GLSL result is undefined (pow of a negative base: NaN in the oracle,
+    scene OG at P7 only) are not compared (tests/test_oracle_golden.py)."""
     z = np.load(path, allow_pickle=False)
     m = json.loads(str(z["meta"]))
     pose = dict(pos=m["pos"], mouse=m["mouse"], time=m["time"])
     setup(R, m["scene"], pose, m["max_steps"])
-    img, st = hip(R, m["W"], m["H"])
-    assert_parity(m["scene"], img, z["rgba"], label="vs golden")
+    img, evmap, st = R.render_step_map(m["W"], m["H"])
+    img, evmap = img.cpu().numpy(), evmap.cpu().numpy()
+    o, ev = ref(m["scene"], m["W"], m["H"], pose, m["max_steps"])
+    ok = ~np.isnan(o[..., :3]).any(-1)
+    sg = assert_parity(m["scene"], img[ok], z["rgba"][ok], label="vs golden")
+    so = assert_parity(m["scene"], img[ok], o[ok], label="vs oracle")
+    exact = float(np.mean(evmap == z["evals"]))
+    print(f"{os.path.basename(path)}: vs golden {sg}, vs oracle {so}, step map exact {exact:.4f}")
+    assert exact >= STEP_MAP_EXACT, exact
+    assert int(evmap.sum(dtype=np.int64)) == st["evals"]
     check_evals(st, z["evals"])
-    o, _ = ref(m["scene"], m["W"], m["H"], pose, m["max_steps"])
-    assert_parity(m["scene"], img, o, label="vs oracle")
 
 
 # per-ray-step FLOP bounds of the instrumented tally (rm_device.h Tally,

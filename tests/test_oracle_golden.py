@@ -1,5 +1,11 @@
 """The CPU oracle against the golden images SwiftShader rendered from the
-reference GLSL (tests/golden/make_goldens.py) -- pins the oracle."""
+reference GLSL (tests/golden/make_goldens.py) -- pins the oracle.
+
+After the attribution of DESIGN.md section 3 (GLSL sin/cos and normalize as
+the fixture renderer evaluates them, exact pixel-centre texture coordinates)
+the oracle reproduces the reference GLSL's images to a few 1e-6 and its
+per-pixel sceneSDF call counts exactly; the scene-O diagnostic fixtures pin
+the intermediate terms (normal, SSS thickness, shadow, reflection bounce)."""
 import glob
 import json
 import os
@@ -8,10 +14,15 @@ import numpy as np
 import pytest
 
 import oracle
-from tests.parity import assert_parity
+from tests.parity import assert_parity, diff_stats
 
 GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
-                if os.path.basename(p).startswith(("S0_", "T_", "O_")))
+                if os.path.basename(p).startswith(("S0_", "T_", "O_", "OG_")))
+DIAG = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "DIAG_*.npz")))
+
+# |oracle - reference GLSL| per channel: the residual is the fixture
+# renderer's pow/exp/log2 (~3e-7 relative, tools/ss_probe.py), not amplified
+MAX_ABS = 1e-4
 
 
 def load(path):
@@ -19,10 +30,19 @@ def load(path):
     return z["rgba"], z["evals"], json.loads(str(z["meta"]))
 
 
+def defined(img):
+    """Pixels whose GLSL result is defined.  Where the oracle's pixel is NaN
+    the reference took pow() of a negative base (glass seen from inside, test
+    scene OG at P7): GLSL leaves that undefined (the fixture renderer returns
+    pow(|x|, y), common GPUs NaN), so those pixels are not compared."""
+    return ~np.isnan(img[..., :3]).any(-1)
+
+
 def test_goldens_present():
     names = {os.path.basename(p)[:-4] for p in GOLDEN}
-    assert {"S0_64_P0", "T_64_P0", "O_64_P0"} <= names
-    assert len(GOLDEN) >= 9
+    assert {"S0_64_P0", "T_64_P0", "O_64_P0", "OG_96x54_P1"} <= names
+    assert len(GOLDEN) >= 12
+    assert len(DIAG) >= 2
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
@@ -31,9 +51,31 @@ def test_oracle_matches_reference_glsl(path):
     img, ev = oracle.render(m["scene"], m["W"], m["H"], pos=m["pos"], mouse=m["mouse"], time=m["time"],
                             max_steps=m["max_steps"])
     assert img.shape == rgba.shape
-    s = assert_parity(m["scene"], img, rgba, label=os.path.basename(path))
-    # the step counts (sceneSDF calls per pixel) of the reference GLSL run
-    assert np.mean(ev == evals) >= 0.99, s
-    assert abs(float(ev.mean()) - float(evals.mean())) / float(evals.mean()) < 2e-3
+    ok = defined(img)
+    assert ok.mean() >= (0.3 if m["pose"] == "P7" else 1.0)
+    s = assert_parity(m["scene"], img[ok], rgba[ok], label=os.path.basename(path))
+    assert s["max"] <= MAX_ABS, s
+    # the per-pixel step counts (sceneSDF calls) of the reference GLSL run
+    np.testing.assert_array_equal(ev, evals)
     # alpha is 1 everywhere (gl_FragColor = vec4(col, 1.0))
     assert np.all(img[..., 3] == 1.0)
+
+
+@pytest.mark.parametrize("path", DIAG, ids=[os.path.basename(p)[:-4] for p in DIAG])
+def test_oracle_intermediate_terms_match_reference_glsl(path):
+    """Term-by-term attribution fixture (make_goldens.py diag_edit): the hit
+    normal, CalculateThickness, the shadow and AO factors and the reflection
+    bounce of every pixel, as the reference GLSL computed them."""
+    z = np.load(path, allow_pickle=False)
+    m = json.loads(str(z["meta"]))
+    g = z["diag"]
+    d, img = oracle.render_diag("O", m["W"], m["H"], pos=m["pos"], mouse=m["mouse"], time=m["time"],
+                                max_steps=m["max_steps"])
+    assert d.shape == g.shape
+    # normals, hit depths, thickness, shadow, AO: bit-exact (they feed Hash33)
+    for k in (0, 1, 3, 4):
+        np.testing.assert_array_equal(d[:, :, k], g[:, :, k], err_msg=f"channel {k}: {m['channels'][k]}")
+    # colours: within the fixture renderer's pow/exp precision
+    for k in (2, 5, 6):
+        assert np.nanmax(np.abs(d[:, :, k] - g[:, :, k])) <= MAX_ABS, m["channels"][k]
+    assert diff_stats(img, z["rgba"])["max"] <= MAX_ABS
