@@ -11,9 +11,13 @@
 //
 // Usage: raymarch_headless [--scene output_shader.frag] [--w 1600] [--h 900]
 //          [--frames 60] [--script WWWWDD..] [--mouse 3,0] [--time-freeze]
-//          [--steps 128] [--ppm out.ppm]
+//          [--steps 128] [--ppm out.ppm] [--gpus N] [--band 16]
+// --gpus N renders each frame's row bands on GPUs 0..N-1 and gathers them over
+// RCCL to GPU 0 (rm::ShardedRenderTexture -> rm_render_sharded_all); --sharded
+// takes that path with one GPU too.
 #include <chrono>
 #include <cmath>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,9 +29,9 @@
 
 int main(int argc, char** argv) {
     std::string scene = "output_shader.frag", script, ppm;
-    int w = 1600, h = 900, frames = 60, steps = 128;
+    int w = 1600, h = 900, frames = 60, steps = 128, gpus = 1, band = 16;
     int mdx = 0, mdy = 0;
-    bool time_freeze = false;
+    bool time_freeze = false, sharded = false;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() { return i + 1 < argc ? std::string(argv[++i]) : std::string(); };
@@ -37,8 +41,11 @@ int main(int argc, char** argv) {
         else if (a == "--frames") frames = std::atoi(next().c_str());
         else if (a == "--script") script = next();
         else if (a == "--steps") steps = std::atoi(next().c_str());
+        else if (a == "--gpus") gpus = std::atoi(next().c_str());
+        else if (a == "--band") band = std::atoi(next().c_str());
         else if (a == "--ppm") ppm = next();
         else if (a == "--time-freeze") time_freeze = true;
+        else if (a == "--sharded") sharded = true;
         else if (a == "--mouse") std::sscanf(next().c_str(), "%d,%d", &mdx, &mdy);
         else {
             std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -52,19 +59,37 @@ int main(int argc, char** argv) {
     rm::Vec3 pos{2.0f, 3.0f, 3.0f};
     int framesStill = 1;
 
+    if (gpus < 1) {
+        std::fprintf(stderr, "--gpus must be >= 1\n");
+        return 2;
+    }
+    // one shader (librm context) per GPU; the first is the reference's `shader`
+    std::vector<std::unique_ptr<rm::Shader>> shaders;
+    std::vector<rm::Shader*> all;
+    for (int g = 0; g < gpus; g++) {
+        shaders.emplace_back(new rm::Shader(g));
+        rm::Shader& s = *shaders.back();
+        if (!s.valid()) {
+            std::fprintf(stderr, "no HIP device %d\n", g);
+            return 1;
+        }
+        if (!rm::ShaderLoader::loadFromFile(scene.c_str(), rm::Shader::Fragment, s)) return 1;
+        s.setUniform("u_resolution", rm::Vec2{wf, hf});
+        s.setMarchSteps(steps);
+        all.push_back(&s);
+    }
+    rm::Shader& shader = *all[0];
+    sharded = sharded || gpus > 1;
+    auto setAll = [&](const char* name, auto v) {
+        for (rm::Shader* s : all) s->setUniform(name, v);
+    };
     rm::RenderTexture outputTexture;
-    if (!outputTexture.create(w, h)) {
-        std::fprintf(stderr, "cannot allocate %dx%d target\n", w, h);
+    rm::ShardedRenderTexture shardedTexture;
+    if (!sharded ? !outputTexture.create(w, h) : !shardedTexture.create(w, h, all, band)) {
+        std::fprintf(stderr, "cannot allocate the %dx%d target on %d GPU(s): %s\n", w, h, gpus,
+                     shader.lastError().c_str());
         return 1;
     }
-    rm::Shader shader;
-    if (!shader.valid()) {
-        std::fprintf(stderr, "no HIP device\n");
-        return 1;
-    }
-    if (!rm::ShaderLoader::loadFromFile(scene.c_str(), rm::Shader::Fragment, shader)) return 1;
-    shader.setUniform("u_resolution", rm::Vec2{wf, hf});
-    shader.setMarchSteps(steps);
 
     std::mt19937 e2(20261015);
     std::uniform_real_distribution<float> dist(0.0f, 1.0f);
@@ -90,30 +115,34 @@ int main(int argc, char** argv) {
         pos = rm::Vec3{pos.x + nx * speed, pos.y + ty * speed, pos.z + nz * speed};
         for (bool b : wasd)
             if (b) framesStill = 1;
-        shader.setUniform("u_pos", pos);
-        shader.setUniform("u_mouse", rm::Vec2{mx, my});
+        setAll("u_pos", pos);
+        setAll("u_mouse", rm::Vec2{mx, my});
         if (!time_freeze) {
             float t = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
-            shader.setUniform("u_time", t);
+            setAll("u_time", t);
         }
-        shader.setUniform("u_sample_part", 1.0f / framesStill);
-        shader.setUniform("u_seed1", rm::Vec2{dist(e2) * 999.0f, dist(e2) * 999.0f});
-        shader.setUniform("u_seed2", rm::Vec2{dist(e2) * 999.0f, dist(e2) * 999.0f});
-        rm_stats st;
-        if (!outputTexture.draw(shader, &st)) {
+        setAll("u_sample_part", 1.0f / framesStill);
+        const rm::Vec2 seed1{dist(e2) * 999.0f, dist(e2) * 999.0f}, seed2{dist(e2) * 999.0f, dist(e2) * 999.0f};
+        setAll("u_seed1", seed1);
+        setAll("u_seed2", seed2);
+        std::vector<rm_stats> st(gpus);
+        if (!sharded ? !outputTexture.draw(shader, st.data()) : !shardedTexture.draw(st.data())) {
             std::fprintf(stderr, "draw failed: %s\n", shader.lastError().c_str());
             return 1;
         }
-        kernel_ms += st.kernel_ms;
+        float slowest = 0.0f;
+        for (const rm_stats& x : st) slowest = x.kernel_ms > slowest ? x.kernel_ms : slowest;
+        kernel_ms += slowest;
         framesStill++;
     }
     double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::printf("{\"frames\": %d, \"w\": %d, \"h\": %d, \"scene\": \"%s\", \"kernel_ms_per_frame\": %.4f, "
-                "\"fps_wall\": %.2f, \"pos\": [%.4f, %.4f, %.4f]}\n",
-                frames, w, h, scene.c_str(), frames ? kernel_ms / frames : 0.0, frames / wall, pos.x, pos.y, pos.z);
+    std::printf("{\"frames\": %d, \"w\": %d, \"h\": %d, \"gpus\": %d, \"scene\": \"%s\", "
+                "\"kernel_ms_per_frame\": %.4f, \"fps_wall\": %.2f, \"pos\": [%.4f, %.4f, %.4f]}\n",
+                frames, w, h, gpus, scene.c_str(), frames ? kernel_ms / frames : 0.0, frames / wall, pos.x, pos.y,
+                pos.z);
     if (!ppm.empty()) {
         std::vector<uint32_t> px;
-        if (!outputTexture.copyToHostRGBA8(shader, px)) return 1;
+        if (!sharded ? !outputTexture.copyToHostRGBA8(shader, px) : !shardedTexture.copyToHostRGBA8(px)) return 1;
         FILE* fp = std::fopen(ppm.c_str(), "wb");
         if (!fp) return 1;
         std::fprintf(fp, "P6\n%d %d\n255\n", w, h);

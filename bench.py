@@ -58,8 +58,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
-    ap.add_argument("--pmc", default=os.path.join(HERE, "profiles", "pmc_traffic.json"),
-                    help="rocprofv3 PMC summary used for roofline.traffic (if it matches the workload)")
+    ap.add_argument("--pmc", default=os.path.join(HERE, "profiles", "pmc_counters.json"),
+                    help="per-workload rocprofv3 PMC counters (profiles/): executed FP32 ops for "
+                         "roofline.achieved, HBM bytes for roofline.traffic, VALU/SALU issue")
     return ap.parse_args()
 
 
@@ -103,15 +104,26 @@ def cpu_baseline(args, pose, W, H, target_s):
                 break
     except OSError:
         pass
+    threads = int(L.oracle_num_threads())
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    omp_env = os.environ.get("OMP_NUM_THREADS")
     return {
         "value": evals / dt,
         "unit": "ray-steps/s",
         "frames_per_s": (len(rows) / H) / dt,
-        "cores": int(L.oracle_num_threads()),
+        "cores": threads,
         "kind": "port",
+        "threads": {"openmp_threads_used": threads, "OMP_NUM_THREADS": omp_env, "sched_affinity_cpus": affinity,
+                    "nproc": os.cpu_count(),
+                    "note": "OpenMP runs OMP_NUM_THREADS threads when it is set (the GPU pool sets it to the "
+                            "per-GPU CPU share and asks runs to keep it), else one per CPU of the affinity mask; "
+                            "nproc counts the whole host"},
         "sample": f"rows y = 0 mod {stride} of the {W}x{H} frame ({len(rows)} rows, {evals} ray-steps, "
                   f"{dt:.2f} s); frames/s extrapolated by row fraction; OpenMP dynamic rows, -O3 "
-                  f"x86-64-v3; host CPU: {model}, nproc={os.cpu_count()}",
+                  f"x86-64-v3; host CPU: {model}, {threads} threads",
     }
 
 
@@ -172,6 +184,44 @@ def time_bloom(r, frame8, stream, reps=20):
             "hbm": {"achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
                     "algorithmic_bytes": nbytes},
             "mip_levels": d2, "texel_fetches_per_px": 4 * (1 + 25 * 2)}
+
+
+def roofline(pmc, flop_tally, evals, ref_flop_per_step, kern_ms, out_bytes):
+    """The render kernel's FP32-VALU roofline.  With PMC counters of this
+    workload (profiles/pmc_counters.json, rocprofv3 --pmc of the same command):
+    executed FP32 FLOP = (ADD + MUL + TRANS + 2 FMA) F32 wave-instructions x 64
+    lanes per launch, over this run's live kernel time.  Without: the
+    instrumented per-term tally (SURVEY.md 8(d) prices over the terms
+    evaluated).  VALU/SALU issue fractions beside it."""
+    t = kern_ms / 1e3
+    keys = ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32")
+    if all(k in pmc for k in keys):
+        flop = 64 * (pmc[keys[0]] + pmc[keys[1]] + pmc[keys[2]] + 2 * pmc[keys[3]])
+        src = f"PMC executed FP32 ops ({pmc.get('source')}): 64 x (ADD + MUL + TRANS + 2 FMA)"
+    else:
+        flop = flop_tally
+        src = "instrumented tally (no PMC counters for this workload in profiles/)"
+    ach = flop / t / 1e12
+    roof = {
+        "bound": "valu", "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": ach / PEAK_FP32_TFLOPS, "traffic": pmc.get("hbm_bytes_per_launch"),
+        "flop_per_launch": flop, "flop_source": src, "ray_steps_per_launch": evals,
+        "tally_flop_per_launch": flop_tally, "tally_tflops": flop_tally / t / 1e12,
+        "reference_tally_flop_per_ray_step": ref_flop_per_step,
+        "reference_equivalent_tflops": evals * ref_flop_per_step / t / 1e12,
+        "hbm": {"achieved": out_bytes / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": out_bytes / t / 1e9 / PEAK_HBM_GBS, "algorithmic_bytes_per_launch": out_bytes},
+    }
+    if "SQ_INSTS_VALU" in pmc:
+        # issue fractions at the clock the PMC run measured (GRBM_GUI_ACTIVE / 8 XCDs / kernel time):
+        # one wave64 VALU instruction per 2 cycles per SIMD (1024 SIMDs), one SALU per cycle per CU (256)
+        clk = pmc.get("clock_hz") or 2.4e9
+        roof["valu_issue"] = {"insts_per_launch": pmc["SQ_INSTS_VALU"],
+                              "frac": pmc["SQ_INSTS_VALU"] * 2 / (t * clk * 1024), "clock_hz": clk}
+        if "SQ_INSTS_SALU" in pmc:
+            roof["salu_issue"] = {"insts_per_launch": pmc["SQ_INSTS_SALU"],
+                                  "frac": pmc["SQ_INSTS_SALU"] / (t * clk * 256)}
+    return roof
 
 
 def main():
@@ -269,7 +319,6 @@ def main():
     if rank == 0:
         F = rm.FLOP_PER_EVAL[args.scene]
         flop_rank = st["flop"]
-        ach = flop_rank / (kern / 1e3) / 1e12
         out_bytes = W * fr.plan.count(0) * (4 if args.fmt == "rgba8" else 16)  # the frame the kernel writes
         pmc = {}
         try:
@@ -278,25 +327,7 @@ def main():
             pmc = pm.get(key, {})
         except (OSError, ValueError):
             pass
-        roof = {
-            "bound": "valu", "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-            "frac": ach / PEAK_FP32_TFLOPS, "traffic": pmc.get("hbm_bytes_per_launch"),
-            "algorithmic_flop_per_launch": flop_rank, "ray_steps_per_launch": evals_rank,
-            "flop_per_ray_step": flop_rank / max(1, evals_rank),
-            "flop_note": "SURVEY.md 8(d) per-term tally over the terms each ray-step evaluates; Menger folds "
-                         "(and scene O's primitives) that an exact early exit skips are not counted",
-            "reference_tally_flop_per_ray_step": F,
-            "reference_equivalent_tflops": evals_rank * F / (kern / 1e3) / 1e12,
-            "hbm": {"achieved": out_bytes / (kern / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": out_bytes / (kern / 1e3) / 1e9 / PEAK_HBM_GBS,
-                    "algorithmic_bytes_per_launch": out_bytes},
-        }
-        if "SQ_INSTS_VALU" in pmc:
-            # executed vector instructions (PMC, per launch) against the issue peak: one wave64
-            # VALU instruction per 2 cycles per SIMD (MI355X_MICROARCH.md), 1024 SIMDs, 2.4 GHz
-            insts = pmc["SQ_INSTS_VALU"]
-            roof["valu_issue"] = {"insts_per_launch": insts, "frac": insts * 2 / (kern / 1e3 * 2.4e9 * 1024),
-                                  "source": pmc.get("source")}
+        roof = roofline(pmc, flop_rank, evals_rank, F, kern, out_bytes)
         res = {
             "metric": "ray-steps/sec + frames/sec at 4096\u00d74096, 1/2/4/8 MI355X",
             "value": evals_frame * args.steps / elapsed,
@@ -320,6 +351,9 @@ def main():
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
             },
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max,
+            "kernel_ms_note": ("per-launch kernel time (HIP events on the render stream)" if len(fr.streams) == 1
+                               else "per-frame stream interval: with 2 streams a frame's events also span the "
+                                    "overlapping frame's kernel; the roofline figures are biased low"),
             "roofline": roof,
         }
         if fr.frame is not None and fr.fmt == "rgba8":

@@ -70,10 +70,17 @@ rm_status rm_destroy(rm_ctx *ctx);
 /* Replaces ShaderLoader::loadFromFile (source/shader_loader.cpp:8-20).
  * If `file_name` exists it is preprocessed with the reference's #include
  * semantics (source/shader_loader.cpp:22-81; missing include -> RM_ERR_FILE).
- * The scene plugin is chosen by the file's base name: "output_shader.frag"
+ * The scene is chosen by the file's base name: "output_shader.frag"
  * (scene O), "template.frag" (scene T, repaired as SURVEY.md App. A),
  * "sphere" (scene S0), "output_shader_glass" (test scene OG).  A registered
- * name needs no file on disk (the GPU host has no shader tree).  Any other
+ * name needs no file on disk (the GPU host has no shader tree).  When the
+ * file exists its text decides (the reference's reload recompiles the edited
+ * shader): output_shader.frag whose lighting/render/main code and included
+ * common.frag are the reference's (whitespace-insensitive fingerprints) loads
+ * the compiled-in scene O if its scene part (materials, floorMat, sceneSDF) is
+ * the reference's too, and otherwise compiles that scene part with hiprtc as
+ * a scene plugin into output_shader.frag's pipeline; other edits (pipeline,
+ * common.frag, template.frag's text) return RM_ERR_SCENE.  Any other
  * existing file named "*.hip" is a scene plugin: a source defining
  * `SdResult sceneSDF(vec3 p)` with the reference's scene library
  * (common.frag:37-679; raymarching_amd/csrc/rm_sdf_lib.h), compiled here with
@@ -83,10 +90,12 @@ rm_status rm_destroy(rm_ctx *ctx);
  * file -> RM_ERR_FILE; another existing file -> RM_ERR_SCENE. */
 rm_status rm_load_scene(rm_ctx *ctx, const char *file_name);
 
-/* Compile a scene plugin without loading it (no GPU needed), as a GL driver
- * compiles a shader: RM_OK, RM_ERR_FILE (missing file or #include) or
- * RM_ERR_SCENE (compile errors).  The compiler's log (NUL-terminated,
- * truncated to log_size) goes to `log` when it is not NULL. */
+/* Compile a scene file as rm_load_scene would, without loading it (no GPU
+ * needed), as a GL driver compiles a shader: RM_OK, RM_ERR_FILE (missing file
+ * or #include) or RM_ERR_SCENE (compile errors, or an edit rm_load_scene
+ * refuses).  The compiler's log, or "compiled-in scene O|T" when no compile is
+ * needed (NUL-terminated, truncated to log_size), goes to `log` when it is not
+ * NULL. */
 rm_status rm_compile_scene(const char *file_name, char *log, size_t log_size);
 
 /* sceneSDF(p) of the loaded scene at n points: points = n xyz float triples,
@@ -190,6 +199,45 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
  * in/out: W x H device buffers, row 0 first, in != out.  Asynchronous on the
  * context's stream. */
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
+
+/* ---- Multi-GPU: row-sharded frames over RCCL ----
+ * The reference renders one frame on one GPU (main.cpp:196-207); here a frame's
+ * rows are dealt to nranks GPUs in bands of `band` rows, round robin (rank r
+ * owns frame row y iff (y / band) % nranks == r).  Each rank renders its rows
+ * (rm_render_band_rgba8), packs them to the 3 B/px RGB8 wire (rm_pack_rgb8),
+ * one ncclGather moves every wire to rank 0 over xGMI, and rank 0 writes the
+ * W x H RGBA8 frame (rm_deinterleave_rgb8).  RCCL (librccl.so.1) is opened at
+ * run time.  A communicator binds a context (its device, stream, scene and
+ * uniforms: set the same uniforms on every rank's context).
+ *
+ * One process per GPU: rank 0 calls rm_comm_get_id and sends the id to the
+ * others out of band (ncclGetUniqueId semantics), then every rank calls
+ * rm_comm_init_rank (collective) and rm_render_sharded per frame (collective;
+ * `frame` is a W*H RGBA8 device buffer on rank 0, ignored elsewhere).
+ * One process driving n GPUs: rm_comm_init_all over n contexts on distinct
+ * devices (ncclCommInitAll; comms[i] is rank i), then rm_render_sharded_all.
+ * Calls are asynchronous on the contexts' streams unless `stats` is given
+ * (then they wait; stats[i].kernel_ms is rank i's render time). */
+typedef struct rm_comm rm_comm;
+typedef struct rm_comm_id {
+    char internal[128]; /* an ncclUniqueId */
+} rm_comm_id;
+/* The layout rm_render_sharded uses (host-only, no GPU): rank `rank` owns
+ * rows_mine frame rows; every rank sends rows_per_shard rows of 3*W bytes
+ * (wire_bytes; rows past rows_mine are padding); rank 0 receives nranks wires
+ * back to back (gathered_bytes), rank r's at offset r * wire_bytes. */
+typedef struct rm_shard_layout {
+    int32_t rows_mine, rows_per_shard;
+    int64_t wire_bytes, gathered_bytes;
+} rm_shard_layout;
+rm_status rm_sharded_layout(int W, int H, int band, int nranks, int rank, rm_shard_layout *out);
+rm_status rm_comm_get_id(rm_comm_id *id);
+rm_status rm_comm_init_rank(rm_comm **comm, rm_ctx *ctx, int nranks, const rm_comm_id *id, int rank);
+rm_status rm_comm_init_all(rm_comm **comms, rm_ctx *const *ctxs, int n);
+rm_status rm_comm_destroy(rm_comm *comm);
+rm_status rm_render_sharded(rm_comm *comm, int W, int H, int band, uint32_t *frame, rm_stats *stats);
+rm_status rm_render_sharded_all(rm_comm *const *comms, int n, int W, int H, int band, uint32_t *frame,
+                                rm_stats *stats);
 
 /* Message of the last failing call on ctx ("" if none). */
 const char *rm_last_error(rm_ctx *ctx);

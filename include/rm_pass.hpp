@@ -34,7 +34,7 @@ class Shader {
 public:
     enum Type { Fragment };
 
-    explicit Shader(int device = 0) {
+    explicit Shader(int device = 0) : device_(device) {
         if (rm_create(&ctx_, device) != RM_OK) ctx_ = nullptr;
     }
     ~Shader() {
@@ -45,6 +45,7 @@ public:
 
     bool valid() const { return ctx_ != nullptr; }
     rm_ctx* ctx() { return ctx_; }
+    int device() const { return device_; }
     std::string lastError() const { return ctx_ ? rm_last_error(ctx_) : "no HIP device"; }
 
     bool setUniform(const char* name, float x) { return ctx_ && rm_set_uniform1f(ctx_, name, x) == RM_OK; }
@@ -64,6 +65,7 @@ public:
 
 private:
     rm_ctx* ctx_ = nullptr;
+    int device_ = 0;
 };
 
 struct ShaderLoader {
@@ -113,6 +115,62 @@ private:
     }
     float* tex_ = nullptr;
     int w_ = 0, h_ = 0;
+};
+
+// The multi-GPU form of RenderTexture::draw: a W x H RGBA8 frame whose row
+// bands are rendered by one Shader per GPU and gathered over RCCL to the first
+// shader's device (rm_comm_init_all + rm_render_sharded_all, one process
+// driving N GPUs).  Set the same uniforms on every shader before draw().
+class ShardedRenderTexture {
+public:
+    ~ShardedRenderTexture() { release(); }
+    bool create(int w, int h, const std::vector<Shader*>& shaders, int band = 16) {
+        release();
+        if (shaders.empty()) return false;
+        std::vector<rm_ctx*> ctxs;
+        for (Shader* s : shaders) {
+            if (!s || !s->valid()) return false;
+            ctxs.push_back(s->ctx());
+        }
+        comms_.assign(ctxs.size(), nullptr);
+        if (rm_comm_init_all(comms_.data(), ctxs.data(), (int)ctxs.size()) != RM_OK) {
+            comms_.clear();
+            return false;
+        }
+        root_ = shaders[0];
+        w_ = w;
+        h_ = h;
+        band_ = band;
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        bool ok = hipSetDevice(root_->device()) == hipSuccess &&
+                  hipMalloc(&frame_, (size_t)w * h * sizeof(uint32_t)) == hipSuccess;
+        (void)hipSetDevice(dev);
+        return ok;
+    }
+    // stats: one rm_stats per GPU (or null)
+    bool draw(rm_stats* stats = nullptr) {
+        return frame_ && rm_render_sharded_all(comms_.data(), (int)comms_.size(), w_, h_, band_, frame_, stats) == RM_OK;
+    }
+    uint32_t* frame() { return frame_; }
+    bool copyToHostRGBA8(std::vector<uint32_t>& out) {
+        out.resize((size_t)w_ * h_);
+        return rm_synchronize(root_->ctx()) == RM_OK && hipSetDevice(root_->device()) == hipSuccess &&
+               hipMemcpy(out.data(), frame_, out.size() * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess;
+    }
+
+private:
+    void release() {
+        for (rm_comm* c : comms_)
+            if (c) rm_comm_destroy(c);
+        comms_.clear();
+        if (frame_) (void)hipFree(frame_);
+        frame_ = nullptr;
+    }
+    std::vector<rm_comm*> comms_;
+    Shader* root_ = nullptr;
+    uint32_t* frame_ = nullptr;
+    int w_ = 0, h_ = 0, band_ = 16;
 };
 
 }  // namespace rm

@@ -23,7 +23,8 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8",
            "rm_pack_rgba8", "rm_pack_rgb8", "rm_deinterleave_rgb8",
            "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_last_error", "rm_status_string",
-           "rm_compile_scene", "rm_scene_eval", "rm_render_step_map")
+           "rm_compile_scene", "rm_scene_eval", "rm_render_step_map", "rm_sharded_layout", "rm_comm_get_id",
+           "rm_comm_init_rank", "rm_comm_init_all", "rm_comm_destroy", "rm_render_sharded", "rm_render_sharded_all")
 
 
 class RmParams(ctypes.Structure):
@@ -38,6 +39,15 @@ class RmStats(ctypes.Structure):
     def as_dict(self):
         return dict(evals=int(self.evals), pixels=int(self.pixels), kernel_ms=float(self.kernel_ms),
                     scene=int(self.scene), flop=int(self.flop))
+
+
+class RmShardLayout(ctypes.Structure):
+    _fields_ = [("rows_mine", ctypes.c_int32), ("rows_per_shard", ctypes.c_int32), ("wire_bytes", ctypes.c_int64),
+                ("gathered_bytes", ctypes.c_int64)]
+
+
+class RmCommId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
 
 
 class RmError(RuntimeError):
@@ -97,6 +107,14 @@ def lib() -> ctypes.CDLL:
         "rm_bloom": ([vp, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_compile_scene": ([cp, vp, c.c_size_t], c.c_int),
         "rm_scene_eval": ([vp, vp, c.c_int64, vp, vp], c.c_int),
+        "rm_sharded_layout": ([c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(RmShardLayout)], c.c_int),
+        "rm_comm_get_id": ([c.POINTER(RmCommId)], c.c_int),
+        "rm_comm_init_rank": ([c.POINTER(vp), vp, c.c_int, c.POINTER(RmCommId), c.c_int], c.c_int),
+        "rm_comm_init_all": ([c.POINTER(vp), c.POINTER(vp), c.c_int], c.c_int),
+        "rm_comm_destroy": ([vp], c.c_int),
+        "rm_render_sharded": ([vp, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
+        "rm_render_sharded_all": ([c.POINTER(vp), c.c_int, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)],
+                                  c.c_int),
         "rm_last_error": ([vp], cp),
         "rm_status_string": ([c.c_int], cp),
     }

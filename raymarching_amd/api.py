@@ -195,6 +195,7 @@ class Renderer:
     def pack_rgb8(self, frame8, out=None):
         """RGBA8 words -> the 3 B/px RGB8 wire (alpha dropped; the pass writes alpha 1)."""
         torch = _torch()
+        _check_out(frame8, frame8.numel())
         npx = frame8.numel()
         if out is None:
             out = torch.empty(tuple(frame8.shape[:-1]) + (3 * frame8.shape[-1],), dtype=torch.uint8,
@@ -206,6 +207,8 @@ class Renderer:
 
     def pack_rgba8(self, frame, out=None):
         torch = _torch()
+        if frame.dtype != torch.float32 or not frame.is_contiguous() or frame.numel() % 4:
+            raise ValueError("pack_rgba8: frame must be a contiguous float32 tensor of RGBA pixels")
         npx = frame.numel() // 4
         if out is None:
             out = torch.empty(frame.shape[:-1], dtype=torch.int32, device=frame.device)
@@ -220,6 +223,8 @@ class Renderer:
         H, W = frame8.shape
         if out is None:
             out = torch.empty_like(frame8)
+        _check_out(frame8, H * W)
+        _check_out(out, H * W)
         check(lib().rm_fxaa(self._ctx, W, H, self._ptr(frame8), self._ptr(out)), self._ctx)
         return out
 
@@ -229,6 +234,8 @@ class Renderer:
         H, W = frame8.shape
         if out is None:
             out = torch.empty_like(frame8)
+        _check_out(frame8, H * W)
+        _check_out(out, H * W)
         check(lib().rm_bloom(self._ctx, W, H, self._ptr(frame8), self._ptr(out)), self._ctx)
         return out
 
@@ -248,12 +255,93 @@ class Renderer:
         torch = _torch()
         if out is None:
             out = torch.empty((H, W), dtype=torch.int32, device=f"cuda:{self.device}")
-        if hasattr(out, "is_cuda"):
-            _check_out(out, H * W)
+        _check_out(out, H * W)
         s = RmStats()
         check(lib().rm_render_rgba8(self._ctx, W, H, self._ptr(out), ctypes.byref(s) if stats else None),
               self._ctx)
         return (out, s.as_dict()) if stats else out
+
+
+def sharded_layout(W: int, H: int, band: int, nranks: int, rank: int) -> dict:
+    """rm_sharded_layout: the row/byte layout of rm_render_sharded (no GPU)."""
+    L = _lib.RmShardLayout()
+    check(lib().rm_sharded_layout(int(W), int(H), int(band), int(nranks), int(rank), ctypes.byref(L)))
+    return dict(rows_mine=L.rows_mine, rows_per_shard=L.rows_per_shard, wire_bytes=L.wire_bytes,
+                gathered_bytes=L.gathered_bytes)
+
+
+def comm_get_id() -> bytes:
+    """rm_comm_get_id (ncclGetUniqueId): rank 0 makes it, every rank passes it to Comm."""
+    cid = _lib.RmCommId()
+    check(lib().rm_comm_get_id(ctypes.byref(cid)))
+    return ctypes.string_at(ctypes.addressof(cid), 128)
+
+
+class Comm:
+    """A librm RCCL communicator bound to a Renderer (rm_comm_*): row-sharded
+    RGBA8 frames, rank r rendering the rows (y // band) % nranks == r and
+    rank 0 receiving the frame (rm_render_sharded)."""
+
+    def __init__(self, renderer: Renderer, nranks: int = 1, rank: int = 0, comm_id: bytes | None = None,
+                 _handle=None):
+        self.r, self.nranks, self.rank = renderer, int(nranks), int(rank)
+        if _handle is not None:
+            self._h = _handle
+            return
+        cid = _lib.RmCommId()
+        if comm_id is not None:
+            ctypes.memmove(ctypes.addressof(cid), comm_id, 128)
+        self._h = ctypes.c_void_p()
+        check(lib().rm_comm_init_rank(ctypes.byref(self._h), renderer._ctx, self.nranks, ctypes.byref(cid),
+                                      self.rank), renderer._ctx)
+
+    @staticmethod
+    def init_all(renderers) -> list:
+        """One process driving len(renderers) GPUs (rm_comm_init_all)."""
+        n = len(renderers)
+        hs = (ctypes.c_void_p * n)()
+        ctxs = (ctypes.c_void_p * n)(*[r._ctx.value for r in renderers])
+        check(lib().rm_comm_init_all(hs, ctxs, n), renderers[0]._ctx)
+        return [Comm(r, n, i, _handle=ctypes.c_void_p(hs[i])) for i, r in enumerate(renderers)]
+
+    def render(self, W: int, H: int, band: int = 16, frame=None, stats: bool = False):
+        """One sharded frame (collective over the ranks).  Rank 0 gets the
+        [H, W] RGBA8 (int32 words) frame, the others None."""
+        torch = _torch()
+        if self.rank == 0 and frame is None:
+            frame = torch.empty((H, W), dtype=torch.int32, device=f"cuda:{self.r.device}")
+        if frame is not None:
+            _check_out(frame, H * W)
+        s = RmStats()
+        check(lib().rm_render_sharded(self._h, int(W), int(H), int(band),
+                                      self.r._ptr(frame) if frame is not None else None,
+                                      ctypes.byref(s) if stats else None), self.r._ctx)
+        return (frame, s.as_dict()) if stats else frame
+
+    @staticmethod
+    def render_all(comms, W: int, H: int, band: int = 16, frame=None, stats: bool = False):
+        """rm_render_sharded_all over the communicators of init_all."""
+        torch = _torch()
+        n = len(comms)
+        if frame is None:
+            frame = torch.empty((H, W), dtype=torch.int32, device=f"cuda:{comms[0].r.device}")
+        _check_out(frame, H * W)
+        hs = (ctypes.c_void_p * n)(*[c._h.value for c in comms])
+        st = (RmStats * n)()
+        check(lib().rm_render_sharded_all(hs, n, int(W), int(H), int(band), comms[0].r._ptr(frame),
+                                          st if stats else None), comms[0].r._ctx)
+        return (frame, [x.as_dict() for x in st]) if stats else frame
+
+    def close(self):
+        if self._h:
+            lib().rm_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
 
 def compile_scene(file_name: str):
@@ -268,7 +356,13 @@ def compile_scene(file_name: str):
 
 
 def _check_out(t, nfloats):
-    if not t.is_contiguous() or t.numel() < nfloats or t.element_size() != 4:
+    """A buffer the C ABI reads or writes as 32-bit words: a contiguous torch
+    tensor or numpy array of 4-byte elements with at least `nfloats` of them."""
+    if hasattr(t, "is_contiguous"):
+        ok, n, es = t.is_contiguous(), t.numel(), t.element_size()
+    else:
+        ok, n, es = bool(t.flags["C_CONTIGUOUS"]), t.size, t.itemsize
+    if not ok or n < nfloats or es != 4:
         raise ValueError(f"buffer must be contiguous 32-bit with >= {nfloats} elements")
 
 

@@ -14,11 +14,14 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <set>
 #include <string>
 
+#include "rm_internal.h"
 #include "rm_launch.h"
 #include "rm_plugin_host.h"
+#include "rm_trace.h"
 
 using rm::FrameConst;
 
@@ -79,6 +82,10 @@ bool preprocess(const std::string &file, std::string &out, std::string &err, int
     }
     std::string line;
     while (std::getline(f, line)) {
+        // text-mode reading as on the reference's platform (MSVC's fstream
+        // turns CRLF into LF): without it the '\r' after a closing quote would
+        // join the include name, since the name loop below re-opens on it
+        if (!line.empty() && line.back() == '\r') line.pop_back();
         size_t found = line.find("#include");
         if (found != std::string::npos && (found == 0 || line.rfind("//", found) == std::string::npos)) {
             std::string name;
@@ -125,6 +132,66 @@ float hash11(float p) {
     float dd = x * (y + 19.19f) + y * (z + 19.19f) + z * (x + 19.19f);
     x += dd; y += dd; z += dd;
     return fract((x + y) * z);
+}
+
+// ---- scene files of registered names (the reference's "Reload scene shader",
+// main.cpp:134-139, recompiles the edited output_shader.frag).  The text is
+// classified by whitespace-insensitive FNV-1a 64 fingerprints of the
+// reference's files (tools/ref_hashes.py; no reference text is kept):
+//   output_shader.frag = prelude (up to the common.frag include) + scene part
+//   (materials, floorMat, sceneSDF) + pipeline (hashes, light, render, main).
+//   Reference prelude/pipeline and library: the scene part is the reference's
+//   -> compiled-in scene O; an edited scene part -> compiled with hiprtc as a
+//   scene plugin into output_shader.frag's pipeline.  An edited pipeline or
+//   common.frag -> RM_ERR_SCENE (only the scene is re-definable).
+//   template.frag: the reference's text -> scene T (repaired),
+//   anything else -> RM_ERR_SCENE.
+constexpr uint64_t kRefCommon = 0xac76e617a4f8cf8fULL;
+constexpr uint64_t kRefTemplate = 0x39cf0bb021dfa9b7ULL;
+constexpr uint64_t kRefOScene = 0x0b0b0c101eafdcf6ULL;
+constexpr uint64_t kRefOFrame = 0x9ebf2dc8811b1dc0ULL;
+
+uint64_t fingerprint(const std::string &t, uint64_t h = 0xcbf29ce484222325ULL) {
+    for (unsigned char c : t) {
+        if (c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\v' || c == '\f') continue;
+        h ^= c;
+        h *= 0x100000001b3ULL;
+    }
+    return h;
+}
+
+bool read_file(const std::string &f, std::string &out) {
+    std::ifstream in(f, std::ios::binary);
+    if (!in.is_open()) return false;
+    out.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+    return true;
+}
+
+// prelude / scene / pipeline of an output_shader.frag-shaped text
+// (tools/ref_hashes.py split_scene); include_name = the first #include's file
+bool split_scene(const std::string &t, std::string &prelude, std::string &scene, std::string &pipeline,
+                 std::string &include_name) {
+    size_t k = t.find("#include");
+    if (k == std::string::npos) return false;
+    size_t e = t.find('\n', k);
+    e = e == std::string::npos ? t.size() : e + 1;
+    size_t a = t.find_first_of("\"<", k), b = a == std::string::npos ? a : t.find_first_of("\">", a + 1);
+    if (a == std::string::npos || b == std::string::npos || b > e) return false;
+    include_name = t.substr(a + 1, b - a - 1);
+    size_t s = t.find("sceneSDF(", e);
+    s = s == std::string::npos ? s : t.find('{', s);
+    if (s == std::string::npos) return false;
+    int depth = 0;
+    for (size_t i = s; i < t.size(); i++) {
+        if (t[i] == '{') depth++;
+        else if (t[i] == '}' && --depth == 0) {
+            prelude = t.substr(0, e);
+            scene = t.substr(e, i + 1 - e);
+            pipeline = t.substr(i + 1);
+            return true;
+        }
+    }
+    return false;
 }
 
 bool is_device_ptr(const void *p) {
@@ -193,6 +260,7 @@ int pick_kernel(const rm_ctx *c) {
 // optional stats (synchronous when given)
 rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, void *out,
                      bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr) {
+    rm::TraceRange range("rm_render");
     FrameConst F = frame_const(ctx, W, H, band, nshards, shard, count);
     F.row0 = row0;
     F.evals_map = evmap;
@@ -260,6 +328,56 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
 
 }  // namespace
 
+namespace {
+
+// Which scene an existing file loads as (see "scene files of registered
+// names" above).  In: sc = the scene of the base name (-1 if none).  Out: sc
+// (SCENE_PLUGIN: compile `src`), src = the plugin source to compile.
+rm_status classify_scene_file(const std::string &file, int &sc, std::string &src, std::string &err) {
+    if (sc < 0) {
+        if (!is_plugin_source(file)) {
+            err = "no HIP scene plugin for \"" + file + "\"";
+            return RM_ERR_SCENE;
+        }
+        sc = rm::SCENE_PLUGIN;
+        return RM_OK;
+    }
+    std::string raw;
+    if (!read_file(file, raw)) {
+        err = "ShaderLoader: can't load file \"" + file + "\"";
+        return RM_ERR_FILE;
+    }
+    if (sc == rm::SCENE_T) {
+        if (fingerprint(raw) == kRefTemplate) return RM_OK;
+        err = "\"" + file + "\" is not the reference's template.frag (which only compiles in its repaired "
+              "form, scene T); write a new scene as a .hip plugin";
+        return RM_ERR_SCENE;
+    }
+    if (sc != rm::SCENE_O) return RM_OK;  // the build's own scene names (S0, OG): no reference text
+    std::string prelude, scene, pipeline, inc, lib;
+    if (!split_scene(raw, prelude, scene, pipeline, inc) || fingerprint(pipeline, fingerprint(prelude)) != kRefOFrame) {
+        err = "\"" + file + "\": only the scene part of output_shader.frag (materials, floorMat, sceneSDF) can "
+              "be redefined; its lighting/render/main code differs from the reference's";
+        return RM_ERR_SCENE;
+    }
+    if (!read_file(inc, lib) || fingerprint(lib) != kRefCommon) {
+        err = "\"" + inc + "\" (included by \"" + file + "\") differs from the reference's common.frag: the "
+              "scene library cannot be redefined; put new helpers in the scene part";
+        return RM_ERR_SCENE;
+    }
+    if (fingerprint(scene) == kRefOScene) return RM_OK;  // the reference's own scene: compiled-in O
+    sc = rm::SCENE_PLUGIN;  // an edited sceneSDF: hiprtc into output_shader.frag's pipeline
+    src = scene;
+    return RM_OK;
+}
+
+}  // namespace
+
+int rm_internal_device(const rm_ctx *ctx) { return ctx->device; }
+hipStream_t rm_internal_stream(const rm_ctx *ctx) { return ctx->stream; }
+int rm_internal_scene(const rm_ctx *ctx) { return ctx->scene; }
+void rm_internal_set_error(rm_ctx *ctx, const std::string &msg) { ctx->err = msg; }
+
 extern "C" {
 
 rm_status rm_create(rm_ctx **out, int device) {
@@ -287,6 +405,7 @@ rm_status rm_create(rm_ctx **out, int device) {
 rm_status rm_destroy(rm_ctx *ctx) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);  // nothing of this context still runs
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
     if (ctx->staging) (void)hipFree(ctx->staging);
@@ -310,8 +429,12 @@ rm_status rm_load_scene(rm_ctx *ctx, const char *file_name) {
             std::fprintf(stderr, "%s\n", err.c_str());
             return fail(ctx, RM_ERR_FILE, err);
         }
-        if (sc < 0) {
-            if (!is_plugin_source(file)) return fail(ctx, RM_ERR_SCENE, "no HIP scene plugin for \"" + file + "\"");
+        rm_status st = classify_scene_file(file, sc, src, err);
+        if (st != RM_OK) {
+            std::fprintf(stderr, "%s\n", err.c_str());
+            return fail(ctx, st, err);
+        }
+        if (sc == rm::SCENE_PLUGIN) {
             // a scene plugin: compiled like the reference's shader reload; on
             // failure the previous scene stays loaded
             rmplugin::Code code;
@@ -321,9 +444,10 @@ rm_status rm_load_scene(rm_ctx *ctx, const char *file_name) {
                 return fail(ctx, RM_ERR_SCENE, "scene plugin \"" + file + "\" failed to compile:\n" + log);
             }
             RM_HIP(hipSetDevice(ctx->device));
+            // kernels of the previous code object may still run on the stream
+            RM_HIP(hipStreamSynchronize(ctx->stream));
             hipError_t e = rmplugin::load(code, ctx->plugin);
             if (e != hipSuccess) return hip_fail(ctx, e, "scene plugin module load");
-            sc = rm::SCENE_PLUGIN;
         }
     } else if (sc < 0) {
         std::string err = "ShaderLoader: can't load file \"" + file + "\"";
@@ -502,6 +626,7 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) 
     if (!is_device_ptr(in) || !is_device_ptr(out))
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_fxaa: device pointers required");
     RM_HIP(hipSetDevice(ctx->device));
+    rm::TraceRange range("rm_fxaa");
     hipError_t e = rm::launch_fxaa(in, out, W, H, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "fxaa launch");
     return RM_OK;
@@ -514,6 +639,7 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
     if (!is_device_ptr(in) || !is_device_ptr(out))
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_bloom: device pointers required");
     RM_HIP(hipSetDevice(ctx->device));
+    rm::TraceRange range("rm_bloom");
     const rm::BloomPlan plan = rm::bloom_plan(W, H);
     if (plan.texels > ctx->mips_texels) {
         if (ctx->mips) RM_HIP(hipFree(ctx->mips));
@@ -559,9 +685,14 @@ rm_status rm_compile_scene(const char *file_name, char *log, size_t log_size) {
     if (!file_name) return RM_ERR_INVALID_ARGUMENT;
     std::string src, err, clog;
     rm_status st = RM_OK;
+    int sc = scene_of(base_name(file_name));
     if (!preprocess(file_name, src, err)) {
         clog = err;
         st = RM_ERR_FILE;
+    } else if ((st = classify_scene_file(file_name, sc, src, err)) != RM_OK) {
+        clog = err;
+    } else if (sc != rm::SCENE_PLUGIN) {
+        clog = "compiled-in scene " + std::string(sc == rm::SCENE_T ? "T" : sc == rm::SCENE_O ? "O" : "(built-in)");
     } else {
         rmplugin::Code code;
         if (!rmplugin::compile(src, file_name, code, clog)) st = RM_ERR_SCENE;

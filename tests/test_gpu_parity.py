@@ -110,18 +110,26 @@ def test_c1_sphere_256(R):
 @pytest.mark.parametrize("pose", list(POSES))
 def test_scene_T_poses(R, pose):
     setup(R, "T", POSES[pose], 128)
-    img, st = hip(R, 192, 108)
+    img, evmap, st = R.render_step_map(192, 108)
+    img, evmap = img.cpu().numpy(), evmap.cpu().numpy()
     o, ev = ref("T", 192, 108, POSES[pose], 128)
-    assert_parity("T", img, o, label=pose)
+    s = assert_parity("T", img, o, label=pose)
+    exact = float(np.mean(evmap == ev))
+    print(f"T {pose} 192x108 vs oracle {s}, step map exact {exact:.4f}")
+    assert exact >= STEP_MAP_EXACT
     check_evals(st, ev)
 
 
 @pytest.mark.parametrize("pose", list(POSES))
 def test_scene_O_poses(R, pose):
     setup(R, "O", POSES[pose], 128)
-    img, st = hip(R, 128, 96)
+    img, evmap, st = R.render_step_map(128, 96)
+    img, evmap = img.cpu().numpy(), evmap.cpu().numpy()
     o, ev = ref("O", 128, 96, POSES[pose], 128)
-    assert_parity("O", img, o, label=pose)
+    s = assert_parity("O", img, o, label=pose)
+    exact = float(np.mean(evmap == ev))
+    print(f"O {pose} 128x96 vs oracle {s}, step map exact {exact:.4f}")
+    assert exact >= STEP_MAP_EXACT
     check_evals(st, ev)
 
 
@@ -130,9 +138,13 @@ def test_glass_variant_refraction_path(R, pose):
     """Test scene OG: blue objects with transparency 0.9 drive renderRefraction
     (output_shader.frag:298-343) and castRayDI (common.frag:903-925)."""
     setup(R, "OG", POSES[pose], 128)
-    img, st = hip(R, 128, 96)
+    img, evmap, st = R.render_step_map(128, 96)
+    img, evmap = img.cpu().numpy(), evmap.cpu().numpy()
     o, ev = ref("OG", 128, 96, POSES[pose], 128)
-    assert_parity("OG", img, o, label=pose)
+    s = assert_parity("OG", img, o, label=pose)
+    exact = float(np.mean(evmap == ev))
+    print(f"OG {pose} 128x96 vs oracle {s}, step map exact {exact:.4f}")
+    assert exact >= STEP_MAP_EXACT
     check_evals(st, ev)
 
 
@@ -319,10 +331,18 @@ def test_shader_loader_surface(torch_cuda, tmp_path, capsys):
     f = tmp_path / "template.frag"
     f.write_text('#include "does_not_exist.frag"\nvoid main() {}\n')
     assert not rm.ShaderLoader.loadFromFile(str(f), rm.Shader.Fragment, sh)
-    # an existing file of a registered name with resolvable includes loads
+    # an existing file of a registered name whose text is not the reference's
+    # is refused (only output_shader.frag's scene part may be redefined), and
+    # the previous scene stays loaded
     (tmp_path / "common.frag").write_text("// library\n")
     f.write_text('#include <' + str(tmp_path / "common.frag") + '>\n// scene T\n')
-    assert rm.ShaderLoader.loadFromFile(str(f), rm.Shader.Fragment, sh)
+    assert not rm.ShaderLoader.loadFromFile(str(f), rm.Shader.Fragment, sh)
+    assert "not the reference's template.frag" in capsys.readouterr().err
+    fo = tmp_path / "output_shader.frag"
+    fo.write_text('#include "' + str(tmp_path / "common.frag") + '"\nSdResult sceneSDF(vec3 p) { return r; }\nvoid main() {}\n')
+    assert not rm.ShaderLoader.loadFromFile(str(fo), rm.Shader.Fragment, sh)
+    tex.draw(sh)
+    assert_parity("O", tex.getTexture().cpu().numpy(), o)  # scene O still loaded
     # an unknown scene file exists but has no HIP plugin
     u = tmp_path / "other.frag"
     u.write_text("void main() {}\n")
@@ -415,6 +435,23 @@ def test_headless_cpp_host_app(tmp_path, torch_cuda):
     ref8 = np.clip(np.rint(np.clip(o[..., :3], 0, 1) * 255.0), 0, 255) / 255.0
     d = np.abs(img - ref8).max(-1)
     assert np.mean(d <= 2.0 / 255.0) >= 0.99, float(np.mean(d <= 2.0 / 255.0))
+
+
+def test_headless_cpp_host_app_sharded_path(tmp_path, torch_cuda):
+    """apps/raymarch_headless --sharded: the frame through rm::ShardedRenderTexture
+    (rm_comm_init_all + rm_render_sharded_all, RGB8 wire) on one GPU equals the
+    plain RenderTexture path's RGBA8 frame byte for byte."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(__file__)), "apps", "raymarch_headless")
+    imgs = []
+    for extra in ([], ["--sharded", "--band", "8"]):
+        ppm = tmp_path / f"f{len(imgs)}.ppm"
+        out = subprocess.run([exe, "--scene", "output_shader.frag", "--w", "80", "--h", "45", "--frames", "3",
+                              "--script", "WD.", "--time-freeze", "--ppm", str(ppm)] + extra,
+                             capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        imgs.append(ppm.read_bytes())
+    assert imgs[0] == imgs[1]
 
 
 def test_render_rows_chunks_and_frame_pipeline(R, torch_cuda):

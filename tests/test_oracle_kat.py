@@ -2,6 +2,7 @@
 semantics of common.frag).  No reference fixtures exist for these; values are
 exact by construction."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -122,3 +123,21 @@ def test_sdbox_equals_componentwise_max(L):
         mc = max(np.float32(abs(x)) - np.float32(1), np.float32(abs(y)) - np.float32(1),
                  np.float32(abs(z)) - np.float32(1))
         assert np.float32(ref) == np.float32(mc), (x, y, z, ref, mc)
+
+
+def test_oracle_under_address_and_undefined_behaviour_sanitizers():
+    """oracle/selftest.c over every scene, the diagnostic channels, FXAA and
+    bloom at ragged sizes, built with -fsanitize=address,undefined (SURVEY.md
+    section 5: sanitizers on the CPU restatement)."""
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    b = subprocess.run(["make", "-C", here, "sanitize"], capture_output=True, text=True)
+    if b.returncode != 0 and "sanitize" in b.stderr and "cannot find" in b.stderr:
+        pytest.skip("no sanitizer runtime")
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ, OMP_NUM_THREADS="4", ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([os.path.join(here, "build", "selftest_asan")], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "selftest ok" in r.stdout

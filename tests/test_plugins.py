@@ -166,8 +166,11 @@ def test_plugin_matches_reference_glsl_golden(R, path):
     z = np.load(path, allow_pickle=False)
     m = json.loads(str(z["meta"]))
     _setup(R, scene_path(m["scene"]), m)
-    img, st = R.render(m["W"], m["H"], stats=True)
-    assert_parity(m["scene"], img.cpu().numpy(), z["rgba"], label="plugin vs golden")
+    img, evmap, st = R.render_step_map(m["W"], m["H"])
+    s = assert_parity(m["scene"], img.cpu().numpy(), z["rgba"], label="plugin vs golden")
+    exact = float(np.mean(evmap.cpu().numpy() == z["evals"]))
+    print(f"{os.path.basename(path)}: plugin vs golden {s}, step map exact {exact:.4f}")
+    assert exact >= 0.95, exact
     tot = int(z["evals"].sum(dtype=np.uint64))
     assert abs(st["evals"] - tot) <= 5e-3 * tot + 4, (st["evals"], tot)
 
@@ -180,8 +183,11 @@ def test_output_shader_plugin_matches_golden(R, name):
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     m = json.loads(str(z["meta"]))
     _setup(R, scene_path("O"), m)
-    img, st = R.render(m["W"], m["H"], stats=True)
-    assert_parity("O", img.cpu().numpy(), z["rgba"], label="plugin O vs golden")
+    img, evmap, st = R.render_step_map(m["W"], m["H"])
+    s = assert_parity("O", img.cpu().numpy(), z["rgba"], label="plugin O vs golden")
+    exact = float(np.mean(evmap.cpu().numpy() == z["evals"]))
+    print(f"{name}: plugin O vs golden {s}, step map exact {exact:.4f}")
+    assert exact >= 0.95, exact
     tot = int(z["evals"].sum(dtype=np.uint64))
     assert abs(st["evals"] - tot) <= 5e-3 * tot + 4, (st["evals"], tot)
 
@@ -225,3 +231,94 @@ def test_failed_reload_keeps_the_previous_scene(R, tmp_path):
         R.load_scene(str(p))
     b = R.render(32, 32).cpu().numpy()
     assert np.array_equal(a, b)
+
+
+# ------------------------------------- reload of the reference's scene files
+
+REF = "/root/reference"  # build container only; these tests skip elsewhere
+
+
+def _ref_tree(tmp_path, edit_scene=None, edit_pipeline=None, edit_common=None):
+    """Copies of the reference's output_shader.frag + common.frag (+ template.frag)
+    in tmp_path, optionally edited the way a user edits them before pressing
+    "Reload scene shader" (main.cpp:134-139)."""
+    src = open(os.path.join(REF, "output_shader.frag")).read()
+    lib = open(os.path.join(REF, "common.frag")).read()
+    if edit_scene:
+        src = edit_scene(src)
+    if edit_pipeline:
+        src = edit_pipeline(src)
+    if edit_common:
+        lib = edit_common(lib)
+    (tmp_path / "output_shader.frag").write_text(src)
+    (tmp_path / "common.frag").write_text(lib)
+    (tmp_path / "template.frag").write_text(open(os.path.join(REF, "template.frag")).read())
+    return tmp_path
+
+
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree absent (GPU box)")
+
+
+@needs_ref
+def test_reference_scene_files_load_the_compiled_in_scenes(tmp_path, monkeypatch):
+    monkeypatch.chdir(_ref_tree(tmp_path))
+    ok, log = rm.compile_scene("output_shader.frag")
+    assert ok and log == "compiled-in scene O", log
+    ok, log = rm.compile_scene("template.frag")
+    assert ok and log == "compiled-in scene T", log
+    # line endings and indentation do not matter
+    (tmp_path / "output_shader.frag").write_text(open(os.path.join(REF, "output_shader.frag")).read()
+                                                 .replace("\n", "\r\n").replace("\t", "    "))
+    ok, log = rm.compile_scene("output_shader.frag")
+    assert ok and log == "compiled-in scene O", log
+
+
+@needs_ref
+def test_edited_scene_part_is_compiled_as_a_plugin(tmp_path, monkeypatch):
+    """The reference's workflow: swap the sponge for the commented mandelbulb
+    line of sceneSDF (output_shader.frag:41-42) and reload."""
+    def edit(s):
+        s = s.replace("\t//SdResult dist0 = SdResult(mandelbulb(", "\tSdResult dist0 = SdResult(mandelbulb(", 1)
+        return s.replace("\tSdResult dist0 = SdResult(mengersponge(", "\t//SdResult dist0 = SdResult(mengersponge(", 1)
+    monkeypatch.chdir(_ref_tree(tmp_path, edit_scene=edit))
+    ok, log = rm.compile_scene("output_shader.frag")
+    assert ok, log
+    assert "compiled-in" not in log
+    # a syntax error in the edited scene is reported with the file's name
+    (tmp_path / "output_shader.frag").write_text(edit(open(os.path.join(REF, "output_shader.frag")).read())
+                                                 .replace("return sminCubic(dist0", "return sminCubic(dist0 +", 1))
+    ok, log = rm.compile_scene("output_shader.frag")
+    assert not ok and "output_shader.frag" in log
+
+
+@needs_ref
+@pytest.mark.parametrize("what", ["pipeline", "common", "template"])
+def test_edits_outside_the_scene_part_are_refused(tmp_path, monkeypatch, what):
+    kw = {}
+    if what == "pipeline":
+        kw["edit_pipeline"] = lambda s: s.replace("float SSSAmbient     = 0.3;", "float SSSAmbient     = 0.5;", 1)
+    elif what == "common":
+        kw["edit_common"] = lambda s: s.replace("const float ZFAR = 50;", "const float ZFAR = 60;", 1)
+    monkeypatch.chdir(_ref_tree(tmp_path, **kw))
+    if what == "template":
+        (tmp_path / "template.frag").write_text(open(os.path.join(REF, "template.frag")).read() + "\n// edit\nint x;\n")
+    ok, log = rm.compile_scene("template.frag" if what == "template" else "output_shader.frag")
+    assert not ok, log
+
+
+@pytest.mark.gpu
+def test_reload_right_after_an_asynchronous_render(R, torch_cuda):
+    """rm_load_scene unloads the previous plugin's code object: it must first
+    wait for kernels of that module still queued on the context's stream."""
+    torch = torch_cuda
+    R.load_scene(scene_path("SC"))
+    R.set_pose((2.0, 3.0, 3.0), (0.0, 0.0), 0.0)
+    R.set_params(max_steps=128, count_evals=0)
+    a = torch.empty((192, 256, 4), dtype=torch.float32, device="cuda")
+    R.render(256, 192, out=a)          # asynchronous: no stats
+    R.load_scene(scene_path("MB"))     # unloads SC's module right away
+    R.render(64, 64)
+    R.load_scene(scene_path("SC"))
+    b = R.render(256, 192)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
