@@ -51,6 +51,10 @@ typedef struct rm_params {
     int32_t shadow_max_steps; /* softshadow2 cap; 0 = unbounded as common.frag:814       */
     int32_t count_evals;      /* 1: instrumented kernel, rm_stats.evals = sceneSDF calls */
     int32_t kernel;           /* workgroup tiling: 0 auto (= 2), 1 16x16 px (4 waves), 2 8x8 px (1 wave), 3 16x4 px (1 wave) */
+    int32_t schedule;         /* dispatch order of one-wave tiles: 1 (default) = the costliest tiles of the previous
+                                 launch of the same geometry on the same stream first (their measured durations,
+                                 counting-sorted on the GPU after each launch); 0 = row-major.  Pixels are the same
+                                 either way; an rm_set_tile_order order takes precedence. */
 } rm_params;
 
 typedef struct rm_stats {
@@ -146,6 +150,18 @@ rm_status rm_render_band(rm_ctx *ctx, int W, int H, int band, int nshards, int s
  * gathered). */
 rm_status rm_render_rows(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
                          float *out, rm_stats *stats);
+
+/* Dispatch order of the render workgroups.  A render launch over W x rows
+ * pixels is a grid of tiles_x x tiles_y tiles (rm_tile_grid: 8x8 pixels per
+ * one-wave workgroup by default); with an order set, workgroup i renders tile
+ * order[i] (tile = ty * tiles_x + tx), for launches whose grid has exactly n
+ * tiles (others keep the identity order).  Pixels are unchanged; only the
+ * time at which each tile starts moves -- e.g. the costliest tiles of the
+ * previous frame first, so that the longest per-pixel chains (grazing soft
+ * shadows) do not start last.  order: host or device, a permutation of
+ * [0, n); n = 0 clears it. */
+rm_status rm_set_tile_order(rm_ctx *ctx, const uint32_t *order, int64_t n);
+rm_status rm_tile_grid(const rm_params *params, int W, int rows, int *tiles_x, int *tiles_y);
 
 /* Number of frame rows shard `shard` owns. */
 rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows);

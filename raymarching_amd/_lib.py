@@ -24,12 +24,13 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_pack_rgba8", "rm_pack_rgb8", "rm_deinterleave_rgb8",
            "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_last_error", "rm_status_string",
            "rm_compile_scene", "rm_scene_eval", "rm_render_step_map", "rm_sharded_layout", "rm_comm_get_id",
-           "rm_comm_init_rank", "rm_comm_init_all", "rm_comm_destroy", "rm_render_sharded", "rm_render_sharded_all")
+           "rm_comm_init_rank", "rm_comm_init_all", "rm_comm_destroy", "rm_render_sharded", "rm_render_sharded_all",
+           "rm_set_tile_order", "rm_tile_grid")
 
 
 class RmParams(ctypes.Structure):
     _fields_ = [("max_steps", ctypes.c_int32), ("shadow_max_steps", ctypes.c_int32),
-                ("count_evals", ctypes.c_int32), ("kernel", ctypes.c_int32)]
+                ("count_evals", ctypes.c_int32), ("kernel", ctypes.c_int32), ("schedule", ctypes.c_int32)]
 
 
 class RmStats(ctypes.Structure):
@@ -115,6 +116,8 @@ def lib() -> ctypes.CDLL:
         "rm_render_sharded": ([vp, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
         "rm_render_sharded_all": ([c.POINTER(vp), c.c_int, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)],
                                   c.c_int),
+        "rm_set_tile_order": ([vp, vp, c.c_int64], c.c_int),
+        "rm_tile_grid": ([c.POINTER(RmParams), c.c_int, c.c_int, c.POINTER(c.c_int), c.POINTER(c.c_int)], c.c_int),
         "rm_last_error": ([vp], cp),
         "rm_status_string": ([c.c_int], cp),
     }

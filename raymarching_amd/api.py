@@ -75,8 +75,11 @@ class Renderer:
         self.set_uniform("u_mouse", *mouse)
         self.set_uniform("u_time", time)
 
-    def set_params(self, max_steps=None, shadow_max_steps=None, count_evals=None, kernel=None) -> None:
+    def set_params(self, max_steps=None, shadow_max_steps=None, count_evals=None, kernel=None,
+                   schedule=None) -> None:
         p = self.params()
+        if schedule is not None:
+            p.schedule = {"adaptive": 1, "rowmajor": 0}.get(schedule, schedule)
         if max_steps is not None:
             p.max_steps = int(max_steps)
         if shadow_max_steps is not None:
@@ -96,6 +99,22 @@ class Renderer:
         """stream: a torch.cuda.Stream, a raw hipStream_t int, or None."""
         raw = getattr(stream, "cuda_stream", stream)
         check(lib().rm_set_stream(self._ctx, ctypes.c_void_p(raw or 0)), self._ctx)
+
+    def tile_grid(self, W: int, rows: int) -> tuple:
+        """(tiles_x, tiles_y) of a render launch over W x rows pixels."""
+        tx, ty = ctypes.c_int(), ctypes.c_int()
+        p = self.params()
+        check(lib().rm_tile_grid(ctypes.byref(p), int(W), int(rows), ctypes.byref(tx), ctypes.byref(ty)))
+        return tx.value, ty.value
+
+    def set_tile_order(self, order=None) -> None:
+        """rm_set_tile_order: workgroup i renders tile order[i] (None clears)."""
+        import numpy as np
+        if order is None:
+            check(lib().rm_set_tile_order(self._ctx, None, 0), self._ctx)
+            return
+        o = np.ascontiguousarray(order, np.uint32)
+        check(lib().rm_set_tile_order(self._ctx, ctypes.c_void_p(o.ctypes.data), len(o)), self._ctx)
 
     def synchronize(self) -> None:
         check(lib().rm_synchronize(self._ctx), self._ctx)

@@ -17,6 +17,7 @@
 #include <iterator>
 #include <set>
 #include <string>
+#include <vector>
 
 #include "rm_internal.h"
 #include "rm_launch.h"
@@ -36,7 +37,7 @@ struct rm_ctx {
     float pos[3] = {0.0f, 0.0f, 0.0f};
     float mouse[2] = {0.0f, 0.0f};
     float time = 0.0f;
-    rm_params params = {128, 0, 0, 0};
+    rm_params params = {128, 0, 0, 0, 1};
     std::string err;
     std::set<std::string> warned;
     unsigned long long *d_evals = nullptr;
@@ -46,6 +47,20 @@ struct rm_ctx {
     uint32_t *mips = nullptr;  // bloom's mip levels 1..d2
     size_t mips_texels = 0;
     rmplugin::Module plugin;  // the loaded scene plugin (scene == SCENE_PLUGIN)
+    uint32_t *tile_order = nullptr;  // rm_set_tile_order (device copy)
+    int64_t tile_order_n = 0;
+    // adaptive dispatch order (rm_params.schedule): per launch geometry and
+    // stream, the tile durations of the last launch and the order they give
+    struct Sched {
+        uint64_t key = 0;
+        hipStream_t stream = nullptr;
+        int n = 0;
+        bool primed = false;       // order holds a permutation from a previous launch
+        uint32_t *buf = nullptr;   // cost[n] | order[n] | scratch[512]
+        uint64_t used = 0;
+    };
+    Sched sched[8];
+    uint64_t sched_clock = 0;
 };
 
 namespace {
@@ -258,12 +273,60 @@ int pick_kernel(const rm_ctx *c) {
 
 // the pass over packed rows [row0, row0 + count) of a shard: device output,
 // optional stats (synchronous when given)
+// The adaptive-order state of a launch geometry on the ctx stream (least
+// recently used entry recycled), or null when scheduling does not apply.
+rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count,
+                          rm_status &st) {
+    st = RM_OK;
+    if (!ctx->params.schedule || ctx->scene == rm::SCENE_PLUGIN || pick_kernel(ctx) != rm::KERNEL_TILE8) return nullptr;
+    const rm::TileGrid g = rm::tile_grid(rm::KERNEL_TILE8, W, count);
+    const int n = g.x * g.y;
+    uint64_t key = 0xcbf29ce484222325ULL;
+    for (long long v : {(long long)ctx->scene, (long long)W, (long long)H, (long long)band, (long long)nshards,
+                        (long long)shard, (long long)row0, (long long)count})
+        key = (key ^ (uint64_t)v) * 0x100000001b3ULL;
+    rm_ctx::Sched *lru = &ctx->sched[0];
+    for (rm_ctx::Sched &e : ctx->sched) {
+        if (e.buf && e.key == key && e.stream == ctx->stream && e.n == n) {
+            e.used = ++ctx->sched_clock;
+            return &e;
+        }
+        if (e.used < lru->used) lru = &e;
+    }
+    if (lru->buf) (void)hipFree(lru->buf);
+    *lru = rm_ctx::Sched();
+    hipError_t e = hipMalloc(&lru->buf, ((size_t)2 * n + 512) * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        lru->buf = nullptr;
+        st = hip_fail(ctx, e, "schedule buffers");
+        return nullptr;
+    }
+    lru->key = key;
+    lru->stream = ctx->stream;
+    lru->n = n;
+    lru->used = ++ctx->sched_clock;
+    return lru;
+}
+
 rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, void *out,
                      bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr) {
     rm::TraceRange range("rm_render");
     FrameConst F = frame_const(ctx, W, H, band, nshards, shard, count);
     F.row0 = row0;
     F.evals_map = evmap;
+    rm_ctx::Sched *sc = nullptr;
+    if (ctx->tile_order && ctx->scene != rm::SCENE_PLUGIN) {  // an explicit order wins
+        const rm::TileGrid g = rm::tile_grid(pick_kernel(ctx), W, count);
+        if ((int64_t)g.x * g.y == ctx->tile_order_n) F.tile_order = ctx->tile_order;
+    } else {
+        rm_status st;
+        sc = sched_slot(ctx, W, H, band, nshards, shard, row0, count, st);
+        if (st != RM_OK) return st;
+        if (sc) {
+            F.tile_cost = sc->buf;
+            if (sc->primed) F.tile_order = sc->buf + sc->n;
+        }
+    }
     bool cnt = ctx->params.count_evals != 0 || evmap;
     if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 2 * sizeof(unsigned long long), ctx->stream));
     if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
@@ -272,8 +335,13 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
             ? rmplugin::launch_render(ctx->plugin, F, out, rgba8, cnt ? ctx->d_evals : nullptr, ctx->stream)
             : rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
+    if (stats) RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    if (sc) {  // this launch's tile durations order the next launch of the geometry (same stream)
+        e = rm::launch_tile_order(sc->buf, sc->n, sc->buf + sc->n, sc->buf + 2 * (size_t)sc->n, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
+        sc->primed = true;
+    }
     if (stats) {
-        RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         RM_HIP(hipEventSynchronize(ctx->ev1));
         float ms = 0.0f;
         RM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -410,6 +478,9 @@ rm_status rm_destroy(rm_ctx *ctx) {
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
     if (ctx->staging) (void)hipFree(ctx->staging);
     if (ctx->mips) (void)hipFree(ctx->mips);
+    if (ctx->tile_order) (void)hipFree(ctx->tile_order);
+    for (rm_ctx::Sched &e : ctx->sched)
+        if (e.buf) (void)hipFree(e.buf);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     delete ctx;
@@ -491,7 +562,8 @@ rm_status rm_set_uniform3f(rm_ctx *ctx, const char *name, float x, float y, floa
 
 rm_status rm_set_params(rm_ctx *ctx, const rm_params *p) {
     if (!ctx || !p) return RM_ERR_INVALID_ARGUMENT;
-    if (p->max_steps < 0 || p->max_steps > (1 << 20) || p->shadow_max_steps < 0 || p->kernel < 0 || p->kernel > 3)
+    if (p->max_steps < 0 || p->max_steps > (1 << 20) || p->shadow_max_steps < 0 || p->kernel < 0 || p->kernel > 3 ||
+        p->schedule < 0 || p->schedule > 1)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_set_params: out of range");
     ctx->params = *p;
     return RM_OK;
@@ -547,6 +619,35 @@ rm_status rm_render_rows_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards,
                                int row_count, uint32_t *out, rm_stats *stats) {
     if (row_count < 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_rows_rgba8: negative row_count");
     return render_any(ctx, W, H, band, nshards, shard, row_begin, row_count, out, true, stats);
+}
+
+rm_status rm_set_tile_order(rm_ctx *ctx, const uint32_t *order, int64_t n) {
+    if (!ctx || n < 0 || (n > 0 && !order)) return RM_ERR_INVALID_ARGUMENT;
+    RM_HIP(hipSetDevice(ctx->device));
+    if (ctx->tile_order) RM_HIP(hipFree(ctx->tile_order));
+    ctx->tile_order = nullptr;
+    ctx->tile_order_n = 0;
+    if (n == 0) return RM_OK;
+    std::vector<uint32_t> h((size_t)n);
+    RM_HIP(hipMemcpy(h.data(), order, (size_t)n * sizeof(uint32_t), hipMemcpyDefault));
+    std::vector<char> seen((size_t)n, 0);  // a permutation of [0, n)
+    for (uint32_t t : h) {
+        if (t >= (uint64_t)n || seen[t]) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_set_tile_order: not a permutation");
+        seen[t] = 1;
+    }
+    RM_HIP(hipMalloc(&ctx->tile_order, (size_t)n * sizeof(uint32_t)));
+    RM_HIP(hipMemcpy(ctx->tile_order, h.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ctx->tile_order_n = n;
+    return RM_OK;
+}
+
+rm_status rm_tile_grid(const rm_params *p, int W, int rows, int *tiles_x, int *tiles_y) {
+    if (!p || !tiles_x || !tiles_y || W <= 0 || rows <= 0) return RM_ERR_INVALID_ARGUMENT;
+    const int k = p->kernel == 1 ? rm::KERNEL_TILE16 : p->kernel == 3 ? rm::KERNEL_TILE16X4 : rm::KERNEL_TILE8;
+    const rm::TileGrid g = rm::tile_grid(k, W, rows);
+    *tiles_x = g.x;
+    *tiles_y = g.y;
+    return RM_OK;
 }
 
 rm_status rm_shard_rows(int H, int band, int nshards, int shard, int *nrows) {

@@ -52,6 +52,8 @@ struct FrameConst {
     float mouse_x, mouse_y;        // u_mouse
     float hash11[32];              // Hash11(i), i = 0..31 (output_shader.frag:54-59,102)
     uint32_t* evals_map;           // instrumented launches: sceneSDF calls per pixel (packed rows), or null
+    const uint32_t* tile_order;    // workgroup i renders tile tile_order[i] (a permutation), or null: tile i
+    uint32_t* tile_cost;           // if set: each one-wave tile's duration in shader clocks (adaptive order)
 };
 
 // A scene plugin's sceneSDF, bound in the plugin's translation unit

@@ -9,6 +9,16 @@
 namespace rm {
 
 
+// the workgroup grid of a render launch over W x rows pixels
+struct TileGrid {
+    int x, y;
+};
+inline TileGrid tile_grid(int kernel, int W, int rows) {
+    const int tw = kernel == KERNEL_TILE16 ? 16 : kernel == KERNEL_TILE16X4 ? 16 : 8;
+    const int th = kernel == KERNEL_TILE16 ? 16 : kernel == KERNEL_TILE16X4 ? 4 : 8;
+    return TileGrid{(W + tw - 1) / tw, (rows + th - 1) / th};
+}
+
 // out: W-wide rows of float4 (rgba8 = false) or RGBA8 words (rgba8 = true)
 hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
                          hipStream_t s);
@@ -23,6 +33,9 @@ hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStrea
 hipError_t launch_pack_rgb8(const uint32_t* in, uint8_t* out, size_t n, hipStream_t s);
 hipError_t launch_deinterleave_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
                                     int rows_per_shard, hipStream_t s);
+// the next launch's tile order (costliest first) from tile durations; scratch:
+// 512 words
+hipError_t launch_tile_order(const uint32_t* cost, int n, uint32_t* order, uint32_t* scratch, hipStream_t s);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 
 // bloom.frag's textureLod level pair and the mip levels 1..d2 it needs,

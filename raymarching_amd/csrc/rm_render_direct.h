@@ -439,9 +439,16 @@ template <int SC, bool COUNT, int K, typename OUT>
 __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict__ out,
                                             unsigned long long* __restrict__ evals) {
     using T = Tiling<K>;
+    const uint64_t t_start = T::WPB == 1 && F.tile_cost ? clock64() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int x = blockIdx.x * T::TW + (w & 1) * 8 + (lane % T::LW);
-    const int j = blockIdx.y * T::TH + (w >> 1) * 8 + (lane / T::LW);
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (F.tile_order) {  // dispatch order != tile order (costliest tiles first, rm_set_tile_order)
+        const uint32_t t = F.tile_order[by * gridDim.x + bx];
+        bx = t % gridDim.x;
+        by = t / gridDim.x;
+    }
+    const int x = bx * T::TW + (w & 1) * 8 + (lane % T::LW);
+    const int j = by * T::TH + (w >> 1) * 8 + (lane / T::LW);
     Tally cnt;
     if (x < F.W && j < F.nrows) {
         const int y = shard_row(F, F.row0 + j);
@@ -452,6 +459,10 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
         c = post_colour<FastMath<SC>::value>(c, tcx, tcy);
         if constexpr (sizeof(OUT) == 4) out[(size_t)j * F.W + x] = pack_rgba8(c.x, c.y, c.z, 1.0f);
         else out[(size_t)j * F.W + x] = make_float4(c.x, c.y, c.z, 1.0f);
+    }
+    if (T::WPB == 1 && F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
+        const uint64_t dt = clock64() - t_start;
+        F.tile_cost[by * gridDim.x + bx] = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;
     }
     if constexpr (COUNT) {
         if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;

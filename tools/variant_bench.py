@@ -23,12 +23,12 @@ sys.path.insert(0, ".")
 import raymarching_amd as rm
 cfgs = json.loads(sys.argv[1])
 r = rm.Renderer(0)
-for name, scene, W, H, steps, pose, band, n, shard in cfgs:
+for (name, scene, W, H, steps, pose, band, n, shard), sched in [(c, s) for c in cfgs for s in (0, 1)]:
     p = rm.POSES[pose]
     r.load_scene(rm.SCENE_FILES[scene])
     r.set_uniform("u_resolution", W, H)
     r.set_pose(p["pos"], p["mouse"], p["time"])
-    r.set_params(max_steps=steps, shadow_max_steps=0, count_evals=1)
+    r.set_params(max_steps=steps, shadow_max_steps=0, count_evals=1, schedule=sched)
     rows = rm.shard_rows(H, band, n, shard)
     out = torch.empty((rows, W), dtype=torch.int32, device="cuda")
     _, st = r.render_band_rgba8(W, H, band, n, shard, out=out, stats=True)
@@ -39,7 +39,7 @@ for name, scene, W, H, steps, pose, band, n, shard in cfgs:
         r.render_band_rgba8(W, H, band, n, shard, out=out)
     torch.cuda.synchronize()
     ms = sorted(r.render_band_rgba8(W, H, band, n, shard, out=out, stats=True)[1]["kernel_ms"] for _ in range(15))
-    print(json.dumps(dict(lib=sys.argv[2], config=name, kernel_ms=ms[len(ms) // 2], min_ms=ms[0],
+    print(json.dumps(dict(lib=sys.argv[2], config=name, schedule=sched, kernel_ms=ms[len(ms) // 2], min_ms=ms[0],
                           ray_steps=evals, rate=evals / (ms[len(ms) // 2] / 1e3))), flush=True)
 '''
 
