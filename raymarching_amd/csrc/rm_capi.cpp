@@ -56,7 +56,8 @@ struct rm_ctx {
         hipStream_t stream = nullptr;
         int n = 0;
         bool primed = false;       // order holds a permutation from a previous launch
-        uint32_t *buf = nullptr;   // cost[n] | order[n] | scratch[512]
+        int parity = 0;            // histogram set the next launch accumulates into
+        uint32_t *buf = nullptr;   // cost[n] | order[n] | 2 x (hist[256] | cursor[256])
         uint64_t used = 0;
     };
     Sched sched[8];
@@ -295,7 +296,8 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
     }
     if (lru->buf) (void)hipFree(lru->buf);
     *lru = rm_ctx::Sched();
-    hipError_t e = hipMalloc(&lru->buf, ((size_t)2 * n + 512) * sizeof(uint32_t));
+    hipError_t e = hipMalloc(&lru->buf, ((size_t)2 * n + 1024) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 2 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->stream);
     if (e != hipSuccess) {
         lru->buf = nullptr;
         st = hip_fail(ctx, e, "schedule buffers");
@@ -324,6 +326,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         if (st != RM_OK) return st;
         if (sc) {
             F.tile_cost = sc->buf;
+            F.tile_hist = sc->buf + 2 * (size_t)sc->n + 512 * sc->parity;
             if (sc->primed) F.tile_order = sc->buf + sc->n;
         }
     }
@@ -337,9 +340,12 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
     if (sc) {  // this launch's tile durations order the next launch of the geometry (same stream)
-        e = rm::launch_tile_order(sc->buf, sc->n, sc->buf + sc->n, sc->buf + 2 * (size_t)sc->n, ctx->stream);
+        uint32_t *h = sc->buf + 2 * (size_t)sc->n;
+        e = rm::launch_tile_order(sc->buf, sc->n, sc->buf + sc->n, h + 512 * sc->parity, h + 512 * (1 - sc->parity),
+                                  ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
         sc->primed = true;
+        sc->parity = 1 - sc->parity;
     }
     if (stats) {
         RM_HIP(hipEventSynchronize(ctx->ev1));

@@ -54,7 +54,17 @@ struct FrameConst {
     uint32_t* evals_map;           // instrumented launches: sceneSDF calls per pixel (packed rows), or null
     const uint32_t* tile_order;    // workgroup i renders tile tile_order[i] (a permutation), or null: tile i
     uint32_t* tile_cost;           // if set: each one-wave tile's duration in shader clocks (adaptive order)
+    uint32_t* tile_hist;           // ... and the histogram of those durations (sched_bucket)
 };
+
+// Buckets of the adaptive dispatch order (rm_capi.cpp, rm_kernels.hip): 256
+// logarithmic buckets of a tile's duration, 8 per octave of shader clocks
+// (float exponent and 3 mantissa bits), bucket 0 = costliest.
+constexpr int kSchedBuckets = 256;
+__device__ __forceinline__ int sched_bucket(uint32_t cost) {
+    const int b = (int)(__float_as_uint((float)cost + 64.0f) >> 20) - ((127 + 6) << 3);
+    return kSchedBuckets - 1 - (b < 0 ? 0 : b > kSchedBuckets - 1 ? kSchedBuckets - 1 : b);
+}
 
 // A scene plugin's sceneSDF, bound in the plugin's translation unit
 // (rm_plugin.h) by specializing this for SCENE_PLUGIN: dist(p), mat(p), flop.

@@ -91,35 +91,19 @@ __global__ __launch_bounds__(256) void rm_deinterleave_rgb8(const uint8_t* __res
 
 // ------------------------------------------------ adaptive dispatch order
 // Next launch's tile order from this launch's tile durations (rm_params.
-// schedule): a counting sort, costliest first, over 256 logarithmic buckets
-// (8 per octave of shader clocks: the float exponent and 3 mantissa bits).
-// Within a bucket the order is arbitrary; the result is a permutation.
-constexpr int kSchedBuckets = 256;
-
-__device__ __forceinline__ int sched_bucket(uint32_t cost) {  // 0 = costliest
-    const int b = (int)(__float_as_uint((float)cost + 64.0f) >> 20) - ((127 + 6) << 3);
-    return kSchedBuckets - 1 - (b < 0 ? 0 : b > kSchedBuckets - 1 ? kSchedBuckets - 1 : b);
-}
-
-// hist[256]: tiles per bucket
-__global__ __launch_bounds__(256) void rm_sched_hist(const uint32_t* __restrict__ cost, int n,
-                                                      uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[kSchedBuckets];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    for (int i = blockIdx.x * 1024 + threadIdx.x; i < min(n, (int)(blockIdx.x + 1) * 1024); i += 256)
-        atomicAdd(&h[sched_bucket(cost[i])], 1u);
-    __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
-}
-
-// each block places its 1024 tiles: bucket offset (exclusive scan of hist) +
-// the block's reservation in the bucket (cursor) + the tile's rank in the block
+// schedule): a counting sort, costliest first, over the sched_bucket buckets
+// (rm_device.h); the render kernel already wrote the durations and their
+// histogram.  Within a bucket the order is arbitrary; the result is a
+// permutation.  Each block places 1024 tiles: bucket offset (exclusive scan
+// of the histogram) + the block's reservation in the bucket (cursor) + the
+// tile's rank in the block.  Block 0 also clears the other launch parity's
+// histogram and cursors (`next`), which the next launch accumulates into.
 __global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restrict__ cost, int n,
                                                          const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor,
-                                                         uint32_t* __restrict__ order) {
+                                                         uint32_t* __restrict__ order, uint32_t* __restrict__ next) {
     __shared__ uint32_t base[kSchedBuckets], cnt[kSchedBuckets];
     const int t = threadIdx.x;
+    if (blockIdx.x == 0) next[t] = next[kSchedBuckets + t] = 0;
     base[t] = hist[t];
     cnt[t] = 0;
     __syncthreads();
@@ -149,14 +133,12 @@ __global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restri
         if (b[k] >= 0) order[base[b[k]] + rank[k]] = (uint32_t)(i0 + 256 * k);
 }
 
-hipError_t launch_tile_order(const uint32_t* cost, int n, uint32_t* order, uint32_t* scratch, hipStream_t s) {
+hipError_t launch_tile_order(const uint32_t* cost, int n, uint32_t* order, uint32_t* hist, uint32_t* next,
+                             hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(scratch, 0, 2 * kSchedBuckets * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
     const unsigned blocks = (unsigned)((n + 1023) / 1024);
-    hipLaunchKernelGGL(rm_sched_hist, dim3(blocks), dim3(256), 0, s, cost, n, scratch);
-    hipLaunchKernelGGL(rm_sched_scatter, dim3(blocks), dim3(256), 0, s, cost, n, scratch, scratch + kSchedBuckets,
-                       order);
+    hipLaunchKernelGGL(rm_sched_scatter, dim3(blocks), dim3(256), 0, s, cost, n, hist, hist + kSchedBuckets, order,
+                       next);
     return hipGetLastError();
 }
 
