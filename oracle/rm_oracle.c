@@ -130,7 +130,9 @@ static inline vec3 normalize3(vec3 a) { return muls(a, 1.0f / length3(a)); }
 static inline float gmin(float x, float y) { return y < x ? y : x; }
 static inline float gmax(float x, float y) { return x < y ? y : x; }
 static inline float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
-static inline float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+/* GLSL mix(x, y, a) (spec: x(1-a) + ya); the pinned implementation (SwiftShader,
+ * tests/golden) evaluates x + (y - x)a (bit-exact on 4096 triples, tools/ss_probe.py) */
+static inline float gmix(float x, float y, float a) { return x + (y - x) * a; }
 static inline vec3 mix3(vec3 x, vec3 y, float a) { return v3(gmix(x.x, y.x, a), gmix(x.y, y.y, a), gmix(x.z, y.z, a)); }
 static inline float gmod(float x, float y) { return x - y * floorf(x / y); }
 static inline float gfract(float x) { return x - floorf(x); }

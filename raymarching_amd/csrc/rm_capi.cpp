@@ -326,7 +326,6 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         if (st != RM_OK) return st;
         if (sc) {
             F.tile_cost = sc->buf;
-            F.tile_hist = sc->buf + 2 * (size_t)sc->n + 512 * sc->parity;
             if (sc->primed) F.tile_order = sc->buf + sc->n;
         }
     }

@@ -54,7 +54,6 @@ struct FrameConst {
     uint32_t* evals_map;           // instrumented launches: sceneSDF calls per pixel (packed rows), or null
     const uint32_t* tile_order;    // workgroup i renders tile tile_order[i] (a permutation), or null: tile i
     uint32_t* tile_cost;           // if set: each one-wave tile's duration in shader clocks (adaptive order)
-    uint32_t* tile_hist;           // ... and the histogram of those durations (sched_bucket)
 };
 
 // Buckets of the adaptive dispatch order (rm_capi.cpp, rm_kernels.hip): 256
@@ -96,7 +95,10 @@ __device__ __forceinline__ V3 normalize(V3 a) { return a * (1.0f / sqrtf(dot(a, 
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
 __device__ __forceinline__ float clamp01(float x) { return gmin(gmax(x, 0.0f), 1.0f); }
-__device__ __forceinline__ float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+// GLSL mix as the implementation that renders the golden fixtures evaluates it:
+// x + (y - x) a (the spec writes x (1 - a) + y a; bit-exact on 4096 triples,
+// tools/ss_probe.py)
+__device__ __forceinline__ float gmix(float x, float y, float a) { return x + (y - x) * a; }
 __device__ __forceinline__ V3 mix3(V3 x, V3 y, float a) {
     return v3(gmix(x.x, y.x, a), gmix(x.y, y.y, a), gmix(x.z, y.z, a));
 }

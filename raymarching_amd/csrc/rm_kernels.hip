@@ -92,12 +92,26 @@ __global__ __launch_bounds__(256) void rm_deinterleave_rgb8(const uint8_t* __res
 // ------------------------------------------------ adaptive dispatch order
 // Next launch's tile order from this launch's tile durations (rm_params.
 // schedule): a counting sort, costliest first, over the sched_bucket buckets
-// (rm_device.h); the render kernel already wrote the durations and their
-// histogram.  Within a bucket the order is arbitrary; the result is a
-// permutation.  Each block places 1024 tiles: bucket offset (exclusive scan
-// of the histogram) + the block's reservation in the bucket (cursor) + the
-// tile's rank in the block.  Block 0 also clears the other launch parity's
-// histogram and cursors (`next`), which the next launch accumulates into.
+// (rm_device.h) of the durations the render kernel wrote.  Within a bucket
+// the order is arbitrary; the result is a permutation.  Two kernels:
+// rm_sched_hist counts tiles per bucket (per-block LDS histograms, one global
+// add per non-empty bucket and block: a global add per tile from the render
+// epilogue instead measured 3x slower frames, 256 hot addresses);
+// rm_sched_scatter places each block's 1024 tiles at bucket offset (exclusive
+// scan of the histogram) + the block's reservation in the bucket (cursor) +
+// the tile's rank in the block, and clears the other parity's histogram and
+// cursors (`next`) for the following launch (no memset on the stream).
+__global__ __launch_bounds__(256) void rm_sched_hist(const uint32_t* __restrict__ cost, int n,
+                                                      uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kSchedBuckets];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int end = min(n, (int)(blockIdx.x + 1) * 1024);
+    for (int i = blockIdx.x * 1024 + threadIdx.x; i < end; i += 256) atomicAdd(&h[sched_bucket(cost[i])], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
 __global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restrict__ cost, int n,
                                                          const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor,
                                                          uint32_t* __restrict__ order, uint32_t* __restrict__ next) {
@@ -137,6 +151,7 @@ hipError_t launch_tile_order(const uint32_t* cost, int n, uint32_t* order, uint3
                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n + 1023) / 1024);
+    hipLaunchKernelGGL(rm_sched_hist, dim3(blocks), dim3(256), 0, s, cost, n, hist);
     hipLaunchKernelGGL(rm_sched_scatter, dim3(blocks), dim3(256), 0, s, cost, n, hist, hist + kSchedBuckets, order,
                        next);
     return hipGetLastError();

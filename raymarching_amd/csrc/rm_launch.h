@@ -33,9 +33,9 @@ hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStrea
 hipError_t launch_pack_rgb8(const uint32_t* in, uint8_t* out, size_t n, hipStream_t s);
 hipError_t launch_deinterleave_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
                                     int rows_per_shard, hipStream_t s);
-// the next launch's tile order (costliest first) from the tile durations and
-// their histogram (hist: 256 counts + 256 cursors, written by the render
-// kernel); clears `next` (512 words) for the following launch
+// the next launch's tile order (costliest first) from the tile durations
+// (hist: 256 counts + 256 cursors, zero on entry); clears `next` (512 words)
+// for the following launch
 hipError_t launch_tile_order(const uint32_t* cost, int n, uint32_t* order, uint32_t* hist, uint32_t* next,
                              hipStream_t s);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);

@@ -462,9 +462,7 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
     }
     if (T::WPB == 1 && F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
         const uint64_t dt = clock64() - t_start;
-        const uint32_t c = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;
-        F.tile_cost[by * gridDim.x + bx] = c;
-        atomicAdd(&F.tile_hist[sched_bucket(c)], 1u);
+        F.tile_cost[by * gridDim.x + bx] = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;
     }
     if constexpr (COUNT) {
         if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;

@@ -108,7 +108,7 @@ __device__ __forceinline__ float sign(float x) { return x > 0.0f ? 1.0f : x < 0.
 __device__ __forceinline__ float min(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float max(float x, float y) { return x < y ? y : x; }
 __device__ __forceinline__ float clamp(float x, float lo, float hi) { return min(max(x, lo), hi); }
-__device__ __forceinline__ float mix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+__device__ __forceinline__ float mix(float x, float y, float a) { return x + (y - x) * a; }  // rm_device.h gmix
 __device__ __forceinline__ float mod(float x, float y) { return x - y * floorf(x / y); }
 __device__ __forceinline__ float fract(float x) { return x - floorf(x); }
 __device__ __forceinline__ float step(float e, float x) { return x < e ? 0.0f : 1.0f; }

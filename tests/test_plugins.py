@@ -139,6 +139,10 @@ def test_scene_library_known_answers(R, kat_file):
         R.set_uniform("u_time", float(i))
         dist, mat = R.scene_eval(pts, material=True)
         rel, ab, allowed = kat.TOL[cls]
+        exact = float(np.mean((dist == z["dist"][i]) & (mat == z["mat"][i]).all(-1)))
+        if exact < 1.0:
+            print(f"LIB_kat {name}: {exact:.3f} of points bit-exact, max |d dist| "
+                  f"{float(np.max(np.abs(dist - z['dist'][i]))):.3g}")
         ok = _within(dist, z["dist"][i], rel, ab) & _within(mat, z["mat"][i], rel, ab).all(-1)
         if int((~ok).sum()) > allowed:
             j = int(np.argmin(ok))
