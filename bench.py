@@ -11,6 +11,11 @@ brings them to rank 0, which de-interleaves the frame.  Total work per step is
 fixed as N grows (strong scaling).  The inputs are uniforms only (synthetic:
 the pose), nothing is read from the host inside the timed region.
 
+Tiles are dispatched costliest first (rm_params.schedule, the default): each
+launch's tile durations order the next launch of the same geometry, so every
+timed frame uses the order measured on the frame before it (the first, untimed
+launches run row-major); --schedule rowmajor turns it off.
+
 value = sceneSDF evaluations (ray-steps) of one frame x steps / wall time of
 the timed region (max over ranks).  The per-frame step count comes from one
 instrumented run of the same kernel (count_evals) before timing; the timed
@@ -55,6 +60,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=None, choices=[1, 2],
                     help="HIP streams frames alternate on (default: 2 for N > 1 over RCCL, else 1)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "tile16", "tile8"])
+    ap.add_argument("--schedule", default="adaptive", choices=["adaptive", "rowmajor"],
+                    help="tile dispatch order: costliest tiles of the previous frame first, or row-major")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
@@ -254,7 +261,7 @@ def main():
     r.load_scene(rm.SCENE_FILES[args.scene])
     r.set_uniform("u_resolution", W, H)
     r.set_pose(pose["pos"], pose["mouse"], pose["time"])
-    r.set_params(max_steps=args.max_steps, shadow_max_steps=0, kernel=args.kernel)
+    r.set_params(max_steps=args.max_steps, shadow_max_steps=0, kernel=args.kernel, schedule=args.schedule)
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream)
     chunks = args.chunks if args.chunks is not None else 1
@@ -309,7 +316,14 @@ def main():
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     live = [c for c in range(nch) if min(fr.cuts[c + 1], fr.nmine) > fr.cuts[c]]  # chunks with rows here
-    kern = sum(evs[i][c][0].elapsed_time(evs[i][c][1]) for i in range(args.steps) for c in live) / args.steps
+    # per-frame interval of the render calls on the frame stream (events around each call: the render
+    # kernel plus the dispatch-order sort it enqueues; with 2 streams it also spans overlapping frames)
+    frame_stream_ms = sum(evs[i][c][0].elapsed_time(evs[i][c][1]) for i in range(args.steps) for c in live) / args.steps
+    # per-launch render-kernel duration (the roofline denominator): synchronous launches of this rank's
+    # rows on the frames' stream, HIP events around the kernel alone (rm_stats.kernel_ms), after the
+    # timed region
+    launch = sorted(fr.render_local(stats=True)[1]["kernel_ms"] for _ in range(11)) if fr.nmine else [0.0]
+    kern = launch[len(launch) // 2]
     kt = torch.tensor([kern], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -347,13 +361,14 @@ def main():
                             f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
                             f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0",
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
-                "band": args.band, "fmt": args.fmt, "wire": fr.wire, "streams": len(fr.streams), "kernel": args.kernel, "chunks": chunks,
+                "band": args.band, "fmt": args.fmt, "wire": fr.wire, "streams": len(fr.streams), "kernel": args.kernel, "chunks": chunks, "schedule": args.schedule,
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
             },
-            "kernel_ms": kern, "kernel_ms_max_rank": kern_max,
-            "kernel_ms_note": ("per-launch kernel time (HIP events on the render stream)" if len(fr.streams) == 1
-                               else "per-frame stream interval: with 2 streams a frame's events also span the "
-                                    "overlapping frame's kernel; the roofline figures are biased low"),
+            "kernel_ms": kern, "kernel_ms_max_rank": kern_max, "frame_stream_ms": frame_stream_ms,
+            "kernel_ms_note": "median per-launch duration of the render kernel (HIP events on its stream, "
+                              "synchronous launches after the timed region, adaptive dispatch order as in the "
+                              "timed frames); frame_stream_ms = mean interval of the timed frames' render calls "
+                              "(kernel + dispatch-order sort; with 2 streams it spans overlapping frames)",
             "roofline": roof,
         }
         if fr.frame is not None and fr.fmt == "rgba8":

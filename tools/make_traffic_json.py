@@ -1,29 +1,44 @@
 #!/usr/bin/env python3
-"""profiles/pmc_traffic.json from a tools/pmc_profile.sh summary.
+"""profiles/pmc_counters.json entry from a tools/pmc_profile.sh summary (the
+counters bench.py's roofline reads for its workload).
 
-HBM bytes per launch of the render kernel = (2 * FETCH_SIZE + WRITE_SIZE) * 1024:
-FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads half the bytes of
-wide coalesced reads (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for
-16-B-per-lane stores (our float4 framebuffer writes).
-usage: make_traffic_json.py SUMMARY.json KEY [KERNEL_SUBSTR] [OUT]
+Per launch of the render kernel:
+  hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  (KiB counters; on
+      gfx950 FETCH_SIZE reads half the bytes of wide coalesced reads,
+      MI355X_MICROARCH.md "HBM"; WRITE_SIZE is exact for the RGBA8 stores,
+      checked against the 64 MiB frame)
+  flop_exec = 64 * (ADD + MUL + TRANS + 2 * FMA) executed F32 wave-instructions
+  clock_hz = GRBM_GUI_ACTIVE / 8 XCDs / the kernel's average duration (from
+      the kernel-trace stats of the same command)
+usage: make_traffic_json.py SUMMARY.json KEY KERNEL_SUBSTR KERNEL_STATS.csv [OUT]
 """
+import csv
 import json
 import os
 import sys
 
-summ, key = sys.argv[1], sys.argv[2]
-ksub = sys.argv[3] if len(sys.argv) > 3 else "rm_render_direct<1, false"
-out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
+summ, key, ksub, stats = sys.argv[1:5]
+out = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_counters.json"
 d = json.load(open(summ))
 k = [n for n in d if ksub in n][0]
 v = d[k]
-entry = {"kernel": k, "FETCH_SIZE_KiB": v["FETCH_SIZE"], "WRITE_SIZE_KiB": v["WRITE_SIZE"],
-         "hbm_bytes_per_launch": (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024,
-         "source": os.path.relpath(summ)}
-for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"):
+avg_ns = [float(r["AverageNs"]) for r in csv.DictReader(open(stats)) if ksub in r["Name"]][0]
+entry = {"kernel": k, "source": os.path.relpath(summ), "kernel_stats": os.path.relpath(stats),
+         "avg_kernel_ns_trace": avg_ns}
+if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+    entry.update(FETCH_SIZE_KiB=v["FETCH_SIZE"], WRITE_SIZE_KiB=v["WRITE_SIZE"],
+                 hbm_bytes_per_launch=(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024)
+for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE", "SQ_INSTS_BRANCH",
+          "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32",
+          "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES"):
     if c in v:
         entry[c] = v[c]
+f32 = ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32")
+if all(c in v for c in f32):
+    entry["flop_exec_per_launch"] = 64 * (v[f32[0]] + v[f32[1]] + v[f32[2]] + 2 * v[f32[3]])
+if "GRBM_GUI_ACTIVE" in v:
+    entry["clock_hz"] = v["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9)
 allj = json.load(open(out)) if os.path.exists(out) else {}
 allj[key] = entry
 json.dump(allj, open(out, "w"), indent=1)
-print(key, entry)
+print(key, json.dumps(entry))
