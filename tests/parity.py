@@ -33,11 +33,10 @@ POLICY = {
     # scene plugins (raymarching_amd/scenes): the mandelbulb's pow/atan/acos
     # orbit is the most ulp-sensitive SDF of the library
     "MB": dict(f2e3=0.9, f1e2=0.97, mean=5e-3),
-    # showcase.hip: more lit surface under output_shader.frag's hashed
-    # sample vectors (fract(x * 443.897), :54-66) than scene O, so more
-    # pixels carry the ulp-amplified noise (measured 93.7 % within 2e-3,
-    # 99.98 % within 1e-2, mean 3e-4 on SC_64_P0)
-    "SC": dict(f2e3=0.92, f1e2=0.995, mean=1e-3),
+    # showcase.hip: its library calls (transformTR, opSmoothUnion, sminCubic,
+    # pMod1, ...) round as the reference GLSL's since mix() is evaluated in the
+    # fixture renderer's form (measured: 100 %, max 7.7e-7)
+    "SC": dict(f2e3=0.99, f1e2=0.999, mean=1e-3),
 }
 
 
