@@ -279,7 +279,8 @@ int pick_kernel(const rm_ctx *c) {
 rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count,
                           rm_status &st) {
     st = RM_OK;
-    if (!ctx->params.schedule || ctx->scene == rm::SCENE_PLUGIN || pick_kernel(ctx) != rm::KERNEL_TILE8) return nullptr;
+    // plugins always launch one-wave 8x8 tiles (rm_plugin_kernels.h)
+    if (!ctx->params.schedule || (ctx->scene != rm::SCENE_PLUGIN && pick_kernel(ctx) != rm::KERNEL_TILE8)) return nullptr;
     const rm::TileGrid g = rm::tile_grid(rm::KERNEL_TILE8, W, count);
     const int n = g.x * g.y;
     uint64_t key = 0xcbf29ce484222325ULL;
@@ -317,8 +318,9 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     F.row0 = row0;
     F.evals_map = evmap;
     rm_ctx::Sched *sc = nullptr;
-    if (ctx->tile_order && ctx->scene != rm::SCENE_PLUGIN) {  // an explicit order wins
-        const rm::TileGrid g = rm::tile_grid(pick_kernel(ctx), W, count);
+    if (ctx->tile_order) {  // an explicit order wins
+        const rm::TileGrid g =
+            rm::tile_grid(ctx->scene == rm::SCENE_PLUGIN ? (int)rm::KERNEL_TILE8 : pick_kernel(ctx), W, count);
         if ((int64_t)g.x * g.y == ctx->tile_order_n) F.tile_order = ctx->tile_order;
     } else {
         rm_status st;

@@ -333,6 +333,7 @@ __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n) {
     return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
 }
 
+
 // Scene distances ("one ray-step" = one call).  EXACT keeps the GLSL's
 // roundings (scene O's marches and normals, whose results feed the normal
 // hash); the fast form serves every other call.

@@ -10,9 +10,12 @@
 
 namespace rm {
 
+#ifndef RM_WAVES_PER_EU
+#define RM_WAVES_PER_EU 1
+#endif
 template <int SC, bool COUNT, int K, typename OUT>
-__global__ __launch_bounds__(64 * Tiling<K>::WPB) void rm_render_direct(FrameConst F, OUT* __restrict__ out,
-                                                                        unsigned long long* __restrict__ evals) {
+__global__ __launch_bounds__(64 * Tiling<K>::WPB) __attribute__((amdgpu_waves_per_eu(RM_WAVES_PER_EU)))
+void rm_render_direct(FrameConst F, OUT* __restrict__ out, unsigned long long* __restrict__ evals) {
     render_tile<SC, COUNT, K, OUT>(F, out, evals);
 }
 

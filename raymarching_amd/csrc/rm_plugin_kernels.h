@@ -22,9 +22,16 @@ struct rm::PluginScene<rm::SCENE_PLUGIN> {
 extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
                                                                   unsigned long long* evals) {
     using namespace rm;
+    const uint64_t t_start = F.tile_cost ? clock64() : 0;
     glsl::plugin_bind_uniforms(F);
     const int lane = threadIdx.x;
-    const int x = blockIdx.x * 8 + (lane & 7), j = blockIdx.y * 8 + (lane >> 3);
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (F.tile_order) {  // costliest tiles first (rm_params.schedule, rm_set_tile_order)
+        const uint32_t t = F.tile_order[by * gridDim.x + bx];
+        bx = t % gridDim.x;
+        by = t / gridDim.x;
+    }
+    const int x = bx * 8 + (lane & 7), j = by * 8 + (lane >> 3);
     Tally cnt;
     if (x < F.W && j < F.nrows) {
         const int y = shard_row(F, F.row0 + j);
@@ -35,6 +42,10 @@ extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst
         const size_t i = (size_t)j * F.W + x;
         if (rgba8) static_cast<uint32_t*>(out)[i] = pack_rgba8(c.x, c.y, c.z, 1.0f);
         else static_cast<float4*>(out)[i] = make_float4(c.x, c.y, c.z, 1.0f);
+    }
+    if (F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
+        const uint64_t dt = clock64() - t_start;
+        F.tile_cost[by * gridDim.x + bx] = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;
     }
     if (evals) {
         if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;

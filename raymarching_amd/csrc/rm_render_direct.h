@@ -229,14 +229,22 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro
     V3 Ld = lightPos - p;
     V3 lightDir = normalize(Ld);
     float occ = ao_real<SC>(F, p, n, cnt);
+#ifdef RM_ABLATE_SHADOW
+    float sha = 1.0f;
+#else
     float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, length(Ld), cnt);
+#endif
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     V3 shading =
         phong<SC>(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, p, ro, lightPos, phongN) * shadow_pow<SC>(sha);
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
+#ifdef RM_ABLATE_SSS
+    float th = 0.5f;
+#else
     float th = thickness<SC>(F, p, n, cnt);
+#endif
     V3 sssl = lightDir + n * 0.6f;
     float sssdot = powf(clamp01(dot(-rd, -sssl)), 1.1f) * 0.3f;
     shading = shading + v3s((sssdot + 0.3f) * th);

@@ -326,3 +326,17 @@ def test_reload_right_after_an_asynchronous_render(R, torch_cuda):
     b = R.render(256, 192)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_plugin_adaptive_dispatch_order_keeps_pixels(R, torch_cuda):
+    """Scene plugins record their tile durations and run costliest first from
+    the second launch on (rm_params.schedule), with the same pixels."""
+    torch = torch_cuda
+    R.load_scene(scene_path("SC"))
+    R.set_pose((2.0, 3.0, 3.0), (0.3, 0.1), 1.5)
+    R.set_params(max_steps=128, count_evals=0, schedule=0)
+    ref = R.render_rgba8(160, 96)
+    R.set_params(schedule=1)
+    for _ in range(3):
+        assert torch.equal(R.render_rgba8(160, 96), ref)

@@ -1,11 +1,13 @@
 #!/bin/bash
-# Build librm.so A/B variants for tools/variant_bench.py: one per RM_OPT mask
-# (rm_device.h), each in its own build directory, into raymarching_amd/variants/.
-# Usage: tools/build_variants.sh MASK [MASK ...]
+# Build librm.so A/B variants for tools/variant_bench.py: each NAME=FLAGS pair
+# (extra device-compile flags, e.g. experiment macros) in its own build
+# directory, into raymarching_amd/variants/librm_NAME.so.
+# Usage: tools/build_variants.sh NAME='-DFOO=1 -DBAR' [NAME=FLAGS ...]
 set -eu
 cd "$(dirname "$0")/../raymarching_amd"
 mkdir -p variants
-for m in "$@"; do
-  make -s B=build/opt$m LIB=variants/librm_opt$m.so EXTRA=-DRM_OPT=$m variants/librm_opt$m.so -j8
+for spec in "$@"; do
+  name=${spec%%=*}; flags=${spec#*=}
+  make -s B=build/v_$name LIB=variants/librm_$name.so EXTRA="$flags" variants/librm_$name.so -j8
 done
 ls -la variants
