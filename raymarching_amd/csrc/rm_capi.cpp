@@ -51,17 +51,22 @@ struct rm_ctx {
     int64_t tile_order_n = 0;
     // adaptive dispatch order (rm_params.schedule): per launch geometry and
     // stream, the tile durations of the last launch and the order they give
+    // Launch k of a geometry writes its tile durations into cost[k & 1]; the
+    // sort of those durations runs on the context's side stream, overlapping
+    // launch k + 1, and writes order[k & 1], which launch k + 2 dispatches
+    // (after waiting for that sort's event).
     struct Sched {
         uint64_t key = 0;
         hipStream_t stream = nullptr;
         int n = 0;
-        bool primed = false;       // order holds a permutation from a previous launch
-        int parity = 0;            // histogram set the next launch accumulates into
-        uint32_t *buf = nullptr;   // cost[n] | order[n] | 2 x (hist[256] | cursor[256])
+        uint64_t k = 0;            // launches so far
+        uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256])
+        hipEvent_t rendered = nullptr, sorted[2] = {nullptr, nullptr};
         uint64_t used = 0;
     };
     Sched sched[8];
     uint64_t sched_clock = 0;
+    hipStream_t side = nullptr;  // the dispatch-order sorts
 };
 
 namespace {
@@ -272,8 +277,20 @@ int pick_kernel(const rm_ctx *c) {
     return rm::KERNEL_TILE8;  // 0 auto, 2: measured fastest on every config
 }
 
-// the pass over packed rows [row0, row0 + count) of a shard: device output,
-// optional stats (synchronous when given)
+// Free an adaptive-order entry once nothing still reads or writes its buffers.
+hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
+    hipError_t r = hipSuccess;
+    if (e.buf) {
+        r = hipStreamSynchronize(e.stream);
+        if (r == hipSuccess && ctx->side) r = hipStreamSynchronize(ctx->side);
+        (void)hipFree(e.buf);
+    }
+    for (hipEvent_t ev : {e.rendered, e.sorted[0], e.sorted[1]})
+        if (ev) (void)hipEventDestroy(ev);
+    e = rm_ctx::Sched();
+    return r;
+}
+
 // The adaptive-order state of a launch geometry on the ctx stream (least
 // recently used entry recycled), or null when scheduling does not apply.
 rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count,
@@ -295,12 +312,15 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
         }
         if (e.used < lru->used) lru = &e;
     }
-    if (lru->buf) (void)hipFree(lru->buf);
-    *lru = rm_ctx::Sched();
-    hipError_t e = hipMalloc(&lru->buf, ((size_t)2 * n + 1024) * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 2 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->stream);
+    hipError_t e = hipSuccess;
+    if (!ctx->side) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = sched_release(ctx, *lru);
+    if (e == hipSuccess) e = hipMalloc(&lru->buf, ((size_t)4 * n + 1024) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 4 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->side);
+    for (hipEvent_t *ev : {&lru->rendered, &lru->sorted[0], &lru->sorted[1]})
+        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
-        lru->buf = nullptr;
+        (void)sched_release(ctx, *lru);
         st = hip_fail(ctx, e, "schedule buffers");
         return nullptr;
     }
@@ -327,8 +347,12 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         sc = sched_slot(ctx, W, H, band, nshards, shard, row0, count, st);
         if (st != RM_OK) return st;
         if (sc) {
-            F.tile_cost = sc->buf;
-            if (sc->primed) F.tile_order = sc->buf + sc->n;
+            const size_t slot = sc->k & 1;
+            F.tile_cost = sc->buf + slot * sc->n;
+            if (sc->k >= 2) {  // the order launch k - 2's durations gave, once its sort has finished
+                RM_HIP(hipStreamWaitEvent(ctx->stream, sc->sorted[slot], 0));
+                F.tile_order = sc->buf + (2 + slot) * sc->n;
+            }
         }
     }
     bool cnt = ctx->params.count_evals != 0 || evmap;
@@ -340,13 +364,16 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
             : rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
-    if (sc) {  // this launch's tile durations order the next launch of the geometry (same stream)
-        uint32_t *h = sc->buf + 2 * (size_t)sc->n;
-        e = rm::launch_tile_order(sc->buf, sc->n, sc->buf + sc->n, h + 512 * sc->parity, h + 512 * (1 - sc->parity),
-                                  ctx->stream);
+    if (sc) {  // sort this launch's durations on the side stream, overlapping the next launch
+        const size_t slot = sc->k & 1;
+        uint32_t *h = sc->buf + 4 * (size_t)sc->n;
+        RM_HIP(hipEventRecord(sc->rendered, ctx->stream));
+        RM_HIP(hipStreamWaitEvent(ctx->side, sc->rendered, 0));
+        e = rm::launch_tile_order(sc->buf + slot * sc->n, sc->n, sc->buf + (2 + slot) * sc->n, h + 512 * slot,
+                                  h + 512 * (1 - slot), ctx->side);
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
-        sc->primed = true;
-        sc->parity = 1 - sc->parity;
+        RM_HIP(hipEventRecord(sc->sorted[slot], ctx->side));
+        sc->k++;
     }
     if (stats) {
         RM_HIP(hipEventSynchronize(ctx->ev1));
@@ -486,8 +513,8 @@ rm_status rm_destroy(rm_ctx *ctx) {
     if (ctx->staging) (void)hipFree(ctx->staging);
     if (ctx->mips) (void)hipFree(ctx->mips);
     if (ctx->tile_order) (void)hipFree(ctx->tile_order);
-    for (rm_ctx::Sched &e : ctx->sched)
-        if (e.buf) (void)hipFree(e.buf);
+    for (rm_ctx::Sched &e : ctx->sched) (void)sched_release(ctx, e);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     delete ctx;

@@ -100,7 +100,8 @@ __global__ __launch_bounds__(256) void rm_deinterleave_rgb8(const uint8_t* __res
 // rm_sched_scatter places each block's 1024 tiles at bucket offset (exclusive
 // scan of the histogram) + the block's reservation in the bucket (cursor) +
 // the tile's rank in the block, and clears the other parity's histogram and
-// cursors (`next`) for the following launch (no memset on the stream).
+// cursors (`next`) for the following sort (no memset on the stream).  The
+// context runs both on a side stream, overlapping the next frame's render.
 __global__ __launch_bounds__(256) void rm_sched_hist(const uint32_t* __restrict__ cost, int n,
                                                       uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[kSchedBuckets];
