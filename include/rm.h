@@ -251,6 +251,9 @@ rm_status rm_comm_get_id(rm_comm_id *id);
 rm_status rm_comm_init_rank(rm_comm **comm, rm_ctx *ctx, int nranks, const rm_comm_id *id, int rank);
 rm_status rm_comm_init_all(rm_comm **comms, rm_ctx *const *ctxs, int n);
 rm_status rm_comm_destroy(rm_comm *comm);
+/* uses_rccl = 1 when the communicator runs RCCL (always for nranks > 1; a
+ * one-rank communicator too whenever librccl loads, else a local copy). */
+rm_status rm_comm_info(const rm_comm *comm, int *nranks, int *rank, int *uses_rccl);
 rm_status rm_render_sharded(rm_comm *comm, int W, int H, int band, uint32_t *frame, rm_stats *stats);
 rm_status rm_render_sharded_all(rm_comm *const *comms, int n, int W, int H, int band, uint32_t *frame,
                                 rm_stats *stats);

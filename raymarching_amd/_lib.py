@@ -25,7 +25,7 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_render_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_last_error", "rm_status_string",
            "rm_compile_scene", "rm_scene_eval", "rm_render_step_map", "rm_sharded_layout", "rm_comm_get_id",
            "rm_comm_init_rank", "rm_comm_init_all", "rm_comm_destroy", "rm_render_sharded", "rm_render_sharded_all",
-           "rm_set_tile_order", "rm_tile_grid")
+           "rm_set_tile_order", "rm_tile_grid", "rm_comm_info")
 
 
 class RmParams(ctypes.Structure):
@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
         "rm_comm_init_rank": ([c.POINTER(vp), vp, c.c_int, c.POINTER(RmCommId), c.c_int], c.c_int),
         "rm_comm_init_all": ([c.POINTER(vp), c.POINTER(vp), c.c_int], c.c_int),
         "rm_comm_destroy": ([vp], c.c_int),
+        "rm_comm_info": ([vp, c.POINTER(c.c_int), c.POINTER(c.c_int), c.POINTER(c.c_int)], c.c_int),
         "rm_render_sharded": ([vp, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
         "rm_render_sharded_all": ([c.POINTER(vp), c.c_int, c.c_int, c.c_int, c.c_int, vp, c.POINTER(RmStats)],
                                   c.c_int),

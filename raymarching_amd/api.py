@@ -308,6 +308,8 @@ class Comm:
             self._h = _handle
             return
         cid = _lib.RmCommId()
+        if comm_id is None and self.nranks == 1:
+            comm_id = comm_get_id()  # a one-rank communicator needs no exchange of the id
         if comm_id is not None:
             ctypes.memmove(ctypes.addressof(cid), comm_id, 128)
         self._h = ctypes.c_void_p()
@@ -350,6 +352,12 @@ class Comm:
         check(lib().rm_render_sharded_all(hs, n, int(W), int(H), int(band), comms[0].r._ptr(frame),
                                           st if stats else None), comms[0].r._ctx)
         return (frame, [x.as_dict() for x in st]) if stats else frame
+
+    @property
+    def uses_rccl(self) -> bool:
+        n, r, u = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().rm_comm_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(u)))
+        return bool(u.value)
 
     def close(self):
         if self._h:

@@ -149,7 +149,7 @@ rm_status enqueue_local(rm_comm *c, int W, int H, int band) {
     if (hipSetDevice(rm_internal_device(ctx)) != hipSuccess) return comm_fail(c, RM_ERR_DEVICE, "hipSetDevice");
     st = grow(c, c->band, c->band_bytes, (size_t)L.rows_per_shard * W * 4);
     if (st == RM_OK) st = grow(c, c->wire, c->wire_bytes, (size_t)L.wire_bytes);
-    if (st == RM_OK && c->rank == 0 && c->nranks > 1) st = grow(c, c->gathered, c->gathered_bytes, (size_t)L.gathered_bytes);
+    if (st == RM_OK && c->rank == 0 && c->nc) st = grow(c, c->gathered, c->gathered_bytes, (size_t)L.gathered_bytes);
     if (st != RM_OK) return st;
     hipStream_t s = rm_internal_stream(ctx);
     if (hipEventRecord(c->ev0, s) != hipSuccess) return comm_fail(c, RM_ERR_DEVICE, "hipEventRecord");
@@ -163,7 +163,7 @@ rm_status enqueue_local(rm_comm *c, int W, int H, int band) {
 
 // the gather of every rank's wire into rank 0's gathered buffer
 rm_status enqueue_gather(rm_comm *c, int W) {
-    if (c->nranks == 1) return RM_OK;  // a one-rank communicator: the wire is the gathered buffer
+    if (!c->nc) return RM_OK;  // a one-rank communicator without RCCL: the wire is the gathered buffer
     rm::TraceRange range("rm_gather");
     Rccl *R = rccl();
     hipStream_t s = rm_internal_stream(c->ctx);
@@ -193,7 +193,7 @@ rm_status finish(rm_comm *c, int W, int H, int band, uint32_t *frame, rm_stats *
     rm::TraceRange range("rm_deinterleave");
     if (c->rank == 0)
         st = rm_deinterleave_rgb8(c->ctx, W, H, band, c->nranks, c->rows_per_shard,
-                                  c->nranks == 1 ? c->wire : c->gathered, frame);
+                                  c->nc ? c->gathered : c->wire, frame);
     if (st != RM_OK || !stats) return st;
     if (hipStreamSynchronize(rm_internal_stream(c->ctx)) != hipSuccess)
         return comm_fail(c, RM_ERR_DEVICE, "hipStreamSynchronize");
@@ -241,7 +241,7 @@ rm_status rm_comm_get_id(rm_comm_id *id) {
 rm_status rm_comm_init_rank(rm_comm **out, rm_ctx *ctx, int nranks, const rm_comm_id *id, int rank) {
     if (!out || !ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return RM_ERR_INVALID_ARGUMENT;
     *out = nullptr;
-    Rccl *R = nranks > 1 ? rccl() : nullptr;  // one rank needs no RCCL
+    Rccl *R = rccl();  // a one-rank communicator goes through RCCL too when it loads
     if (nranks > 1 && !R) {
         rm_internal_set_error(ctx, "rm_comm_init_rank: RCCL unavailable");
         return RM_ERR_DEVICE;
@@ -249,7 +249,7 @@ rm_status rm_comm_init_rank(rm_comm **out, rm_ctx *ctx, int nranks, const rm_com
     rm_comm *c = nullptr;
     rm_status st = comm_new(&c, ctx, nranks, rank);
     if (st != RM_OK) return st;
-    if (nranks > 1) {
+    if (R) {
         ncclUniqueId u;
         std::memcpy(u.internal, id->internal, sizeof(u.internal));
         st = nccl_check(c, R->CommInitRank(&c->nc, nranks, u, rank), "ncclCommInitRank");
@@ -269,7 +269,7 @@ rm_status rm_comm_init_all(rm_comm **comms, rm_ctx *const *ctxs, int n) {
         comms[i] = nullptr;
         if (!ctxs[i]) return RM_ERR_INVALID_ARGUMENT;
     }
-    Rccl *R = n > 1 ? rccl() : nullptr;
+    Rccl *R = rccl();
     if (n > 1 && !R) {
         rm_internal_set_error(ctxs[0], "rm_comm_init_all: RCCL unavailable");
         return RM_ERR_DEVICE;
@@ -277,7 +277,7 @@ rm_status rm_comm_init_all(rm_comm **comms, rm_ctx *const *ctxs, int n) {
     std::vector<int> devs(n);
     std::vector<ncclComm_t> nc(n, nullptr);
     for (int i = 0; i < n; i++) devs[i] = rm_internal_device(ctxs[i]);
-    if (n > 1) {
+    if (R) {
         ncclResult_t r = R->CommInitAll(nc.data(), n, devs.data());
         if (r != 0) {
             rm_internal_set_error(ctxs[0], std::string("ncclCommInitAll: ") +
@@ -316,6 +316,14 @@ rm_status rm_comm_destroy(rm_comm *c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
+    return RM_OK;
+}
+
+rm_status rm_comm_info(const rm_comm *comm, int *nranks, int *rank, int *uses_rccl) {
+    if (!comm) return RM_ERR_INVALID_ARGUMENT;
+    if (nranks) *nranks = comm->nranks;
+    if (rank) *rank = comm->rank;
+    if (uses_rccl) *uses_rccl = comm->nc != nullptr;
     return RM_OK;
 }
 

@@ -109,11 +109,13 @@ def test_one_rank_communicator_equals_render_rgba8(torch_cuda, W, H, band):
     r.set_pose(POSE["pos"], POSE["mouse"], POSE["time"])
     r.set_params(max_steps=128, count_evals=0)
     ref = r.render_rgba8(W, H)
-    c = rm.Comm(r, 1, 0, None)
+    c = rm.Comm(r, 1, 0, rm.comm_get_id())
+    assert c.uses_rccl  # ncclCommInitRank + ncclGather over a one-rank communicator
     frame, st = c.render(W, H, band, stats=True)
     assert torch.equal(frame, ref)
     assert st["pixels"] == W * H and st["kernel_ms"] > 0
     (c1,) = rm.Comm.init_all([r])
+    assert c1.uses_rccl  # ncclCommInitAll
     f1 = rm.Comm.render_all([c1], W, H, band)
     torch.cuda.synchronize()
     assert torch.equal(f1, ref)
