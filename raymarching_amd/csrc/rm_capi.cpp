@@ -155,6 +155,22 @@ float hash11(float p) {
     return fract((x + y) * z);
 }
 
+// (sampleDir * Hash11(i)).y of CalculateThickness (output_shader.frag:75-109)
+// at a normal (0, ny, 0): Hash33 (:61-66), GenerateSampleVector, reflectVector
+// (:70-80) in GLSL float semantics (no contraction; normalize = x * (1/length))
+float sss_floor_term(float ny, int i) {
+    const float fi = (float)i, nx = -0.0f, nyn = -ny, nz = -0.0f;  // -norm
+    float x = fract((nx + fi) * 443.897f), y = fract((nyn + fi) * 441.423f), z = fract((nz + fi) * 437.195f);
+    const float dd = x * (y + 19.19f) + y * (x + 19.19f) + z * (z + 19.19f);  // dot(p3, p3.yxz + 19.19)
+    x += dd; y += dd; z += dd;
+    const float hx = fract((x + y) * z) - 0.5f, hy = fract((x + x) * y) - 0.5f, hz = fract((y + x) * x) - 0.5f;
+    const float r = 1.0f / std::sqrt(hx * hx + hy * hy + hz * hz);
+    const float rx = hx * r, ry = hy * r, rz = hz * r;
+    const float d = rx * nx + ry * nyn + rz * nz;
+    const float dir_y = ry - (nyn * 2.0f) * (d < 0.0f ? d : 0.0f);
+    return dir_y * hash11(fi);
+}
+
 // ---- scene files of registered names (the reference's "Reload scene shader",
 // main.cpp:134-139, recompiles the edited output_shader.frag).  The text is
 // classified by whitespace-insensitive FNV-1a 64 fingerprints of the
@@ -248,7 +264,11 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int
     F.max_steps = c->params.max_steps;
     // 0 (unbounded, the reference) travels as INT_MAX: one compare per shadow step
     F.shadow_max_steps = c->params.shadow_max_steps > 0 ? c->params.shadow_max_steps : 0x7fffffff;
-    for (int i = 0; i < 32; i++) F.hash11[i] = hash11((float)i);
+    for (int i = 0; i < 32; i++) {
+        F.hash11[i] = hash11((float)i);
+        F.sss_floor[0][i] = sss_floor_term(1.0f, i);
+        F.sss_floor[1][i] = sss_floor_term(0x1.fffffep-1f, i);
+    }
     return F;
 }
 

@@ -51,6 +51,8 @@ struct FrameConst {
     float time;                    // u_time
     float mouse_x, mouse_y;        // u_mouse
     float hash11[32];              // Hash11(i), i = 0..31 (output_shader.frag:54-59,102)
+    float sss_floor[2][32];        // CalculateThickness at a floor point whose probes are all plane-only and
+                                   // whose normal is (0, 1, 0) / (0, 1 - 2^-24, 0): (sampleDir * Hash11(i)).y
     uint32_t* evals_map;           // instrumented launches: sceneSDF calls per pixel (packed rows), or null
     const uint32_t* tile_order;    // workgroup i renders tile tile_order[i] (a permutation), or null: tile i
     uint32_t* tile_cost;           // if set: each one-wave tile's duration in shader clocks (adaptive order)
@@ -302,11 +304,21 @@ __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
 // scene O's sceneSDF distance (output_shader.frag:38-48) at world point p with
 // q = its sponge-space image (given by the caller: sponge_space(p), or the
 // sponge-space ray of a march)
+//
+// slack = min(lb - 0.0834 - (d3 + 0.51), mc - (d3 + 0.34)): where it is >= 0
+// both skips below fire and the result is the plane's p.y bit for bit.  Each
+// term is 1-Lipschitz in the Chebyshev norm of a displacement (lb in world
+// space, mc in sponge space, a rotation: <= the Euclidean norm) plus the
+// displacement's |y| (d3; t2 <= d3 for the sponge test), so at p + u the
+// result is still p'.y while |u|_2 + |u_y| <= slack.  The skips have 0.01 of
+// margin over what exactness needs; rounding of the extrapolation is ~1e-5.
+// Callers use it to replace whole spans of rays and whole probe sets of a
+// shading point by the plane (PlaneSpan, rm_render_direct.h).
 template <bool EXACT>
-__device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n) {
+__device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n, float& slack) {
     n.evals++;
-    float d3 = p.y;
-    float m, t2;
+    const float d3 = p.y;
+    float m;
     // Lower bounds of the sphere and the cube (Chebyshev <= Euclidean
     // distance, exactly also after rounding), and sminCubic lowers the min
     // by at most k/6: if even the bound of t1 is past the floor by more than
@@ -314,23 +326,45 @@ __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n) {
     float lb1 = fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))) - 1.0f;
     float lb2 = fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f))) - 1.0f;
     n.flop += FL_BOUNDS + FL_BOX + 1;
-    if (fminf(lb1, lb2) - 0.0834f >= d3 + 0.51f) {
-        t2 = d3;
-    } else {
-        n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
-        float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
-        float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
-        float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
-        t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
-    }
+    const float lbs = fminf(lb1, lb2) - 0.0834f;
+    const float mc = sponge_box(q);
+    slack = fminf(lbs - (d3 + 0.51f), mc - (d3 + 0.34f));
     // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width
     // k = 0.33 (with a margin far above rounding), sminCubic's h is 0 and the
     // result is exactly t2: the sponge's folds are not needed.
-    float mc = sponge_box(q);
-    if (mc >= t2 + 0.34f) return t2;
-    float d0 = sponge_folds<EXACT>(q, mc, n.flop);
+    if (lbs >= d3 + 0.51f) {  // t2 = the plane
+        if (mc >= d3 + 0.34f) return d3;
+        const float d0 = sponge_folds<EXACT>(q, mc, n.flop);
+        n.flop += FL_SMIN;
+        return smin_cubic_d<EXACT>(d0, d3, 0.33f, m);
+    }
+    // Conversely t2 >= A = min(lb - k/6, plane) - k/6 (each sminCubic lowers
+    // a min by at most 0.5/6): where the sponge is below A by more than its
+    // blend width, the result is exactly d0 and the sphere, the cube and their
+    // two blends are not needed (near the sponge, where the folds cost most).
+    const float A = fminf(lbs, d3) - 0.0834f;
+    float d0 = mc;
+    const bool folded = mc + 0.34f <= A;
+    if (folded) {
+        d0 = sponge_folds<EXACT>(q, mc, n.flop);
+        if (d0 + 0.34f <= A) return d0;
+    }
+    n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
+    const float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
+    const float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+    const float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
+    const float t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);
+    if (!folded) {
+        if (mc >= t2 + 0.34f) return t2;
+        d0 = sponge_folds<EXACT>(q, mc, n.flop);
+    }
     n.flop += FL_SMIN;
     return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
+}
+template <bool EXACT>
+__device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n) {
+    float slack;
+    return scene_dist_O<EXACT>(p, q, n, slack);
 }
 
 

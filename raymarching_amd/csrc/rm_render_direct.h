@@ -48,14 +48,47 @@ __device__ __forceinline__ V3 mnormalize(V3 a) {
     else return normalize(a);
 }
 
+// Scene O's floor-plane spans (scene_dist_O's slack, rm_device.h).  Along a
+// ray with a unit direction d the plane-only result holds for a parameter span
+// slack / (1 + |d.y|) (1.01: directions up to 1 % off unit length); the probes
+// of a shading point (normal 0.0018, AO <= 0.8, thickness < 1 away) are all
+// plane-only when the slack there is >= 2.05.
+template <int SC>
+constexpr bool kPlaneSpans = SC == SCENE_O || SC == SCENE_OG;
+__device__ __forceinline__ float plane_rate(V3 d) { return 1.0f / (1.01f + fabsf(d.y)); }
+template <int SC>
+__device__ __forceinline__ bool plane_probes(const FrameConst& F, V3 p) {
+    if constexpr (kPlaneSpans<SC>) {
+        Tally scratch;  // (not a ray-step of the reference)
+        float slack;
+        (void)scene_dist_O<false>(p, sponge_space<false>(F, p), scratch, slack);
+        return slack >= 2.05f;
+    } else {
+        (void)F; (void)p;
+        return false;
+    }
+}
+// a probe's distance: EXACT = the march form (normals), else the probe form
+template <int SC, bool EXACT>
+__device__ __forceinline__ float dist_at(const FrameConst& F, V3 p, Tally& cnt, bool plane) {
+    if constexpr (kPlaneSpans<SC>) {
+        if (plane) {
+            cnt.evals++;
+            return p.y;
+        }
+    }
+    if constexpr (EXACT) return dist_march<SC>(F, p, cnt);
+    else return dist_probe<SC>(F, p, cnt);
+}
+
 // common.frag:697-708 (tetrahedral gradient, h = 0.001)
 template <int SC>
-__device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt) {
+__device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt, bool plane = false) {
     const float h = 0.001f;
-    float d0 = dist_march<SC>(F, p + v3(h, -h, -h), cnt);
-    float d1 = dist_march<SC>(F, p + v3(-h, -h, h), cnt);
-    float d2 = dist_march<SC>(F, p + v3(-h, h, -h), cnt);
-    float d3 = dist_march<SC>(F, p + v3(h, h, h), cnt);
+    float d0 = dist_at<SC, true>(F, p + v3(h, -h, -h), cnt, plane);
+    float d1 = dist_at<SC, true>(F, p + v3(-h, -h, h), cnt, plane);
+    float d2 = dist_at<SC, true>(F, p + v3(-h, h, -h), cnt, plane);
+    float d3 = dist_at<SC, true>(F, p + v3(h, h, h), cnt, plane);
     V3 g = v3(d0, -d0, -d0) + v3(-d1, -d1, d1);
     g = g + v3(-d2, d2, -d2);
     g = g + v3(d3, d3, d3);
@@ -71,6 +104,35 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
     float depth = ZNEAR;
     float res = 0.0f;
     bool hit = false;
+    if constexpr (kPlaneSpans<SC>) {
+        // depth < t_plane: sceneSDF is the floor plane, (ro + rd depth).y
+        const float ia = plane_rate(rd);
+        float t_plane = 0.0f, last = 0.0f;
+        for (int i = 0; i < F.max_steps; i++) {
+            if (depth < t_plane) {
+                res = ro.y + rd.y * depth;
+                cnt.evals++;
+                cnt.flop += 2;
+            } else {
+                V3 q = ro + rd * depth;
+                float slack;
+                cnt.flop += FL_TRANSFORM;
+                res = scene_dist_O<true>(q, sponge_space<true>(F, q), cnt, slack);
+                t_plane = depth + slack * ia;
+            }
+            last = depth;
+            if (INSIDE) {
+                hit = -res < 0.001f * depth;
+                depth = hit ? depth : depth - res;
+            } else {
+                hit = res < 0.001f * depth;
+                depth = hit ? depth : depth + res;
+            }
+            if (hit | (depth >= ZFAR)) break;
+        }
+        last_q = ro + rd * last;  // the point of the last step (ro without steps)
+        return hit ? depth : depth >= ZFAR ? -1.0f : res;
+    }
     last_q = ro;
     for (int i = 0; i < F.max_steps; i++) {
         V3 q = ro + rd * depth;
@@ -97,12 +159,20 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
     const LinRay w{ro, rd}, s = sponge_ray(F, ro, rd);
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
     float t = mint;
+    const float ia = plane_rate(rd);
+    float t_plane = 0.0f;  // t < t_plane: sceneSDF is the floor plane (O/OG)
     for (int it = 1; it == 1 ? t < maxt : true; it++) {
         if constexpr (SC == SCENE_PLUGIN) {
             h = dist_probe<SC>(F, at(w, t), cnt);
+        } else if (t < t_plane) {
+            h = fmaf(w.d.y, t, w.o.y);  // at(w, t).y
+            cnt.evals++;
+            cnt.flop += 2;
         } else {
+            float slack;
             cnt.flop += FL_LINRAY;
-            h = scene_dist_O<false>(at(w, t), at(s, t), cnt);
+            h = scene_dist_O<false>(at(w, t), at(s, t), cnt, slack);
+            t_plane = t + slack * ia;
         }
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
@@ -167,12 +237,12 @@ __device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s
 
 // common.frag:850-866
 template <int SC>
-__device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tally& cnt) {
+__device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tally& cnt, bool plane = false) {
     float sum = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         V3 p = pos + (n * (float)(i + 1)) * 0.2f;
-        sum += (1.0f / (float)(1 << i)) * dist_probe<SC>(F, p, cnt);
+        sum += (1.0f / (float)(1 << i)) * dist_at<SC, false>(F, p, cnt, plane);
     }
     // maxSum = sum_i 2^-i (i+1) 0.2, accumulated in f32 as the reference does
     float maxSum = 0.0f;
@@ -205,7 +275,21 @@ __device__ __forceinline__ V3 shadow_pow(float sha) {
 
 // output_shader.frag:85-116
 template <int SC>
-__device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm, Tally& cnt) {
+__device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm, Tally& cnt, bool plane) {
+    if constexpr (kPlaneSpans<SC>) {
+        // A floor point whose probes are all plane-only: every sample is
+        // pos.y + (sampleDir * sampleLength).y, and the sample directions depend
+        // on the normal alone, which the floor's tetrahedral gradient makes
+        // exactly (0, 1, 0) or (0, 1 - 2^-24, 0): per-frame tables (the host
+        // evaluates GenerateSampleVector in GLSL float semantics).
+        const bool n1 = norm.y == 1.0f;
+        if (plane && norm.x == 0.0f && norm.z == 0.0f && (n1 || norm.y == 0x1.fffffep-1f)) {
+            float th = 0.0f;
+            for (int i = 0; i < 32; i++) th += F.hash11[i] + (pos.y + (n1 ? F.sss_floor[0][i] : F.sss_floor[1][i]));
+            cnt.evals += 32;
+            return clamp01(th * 0.03125f);
+        }
+    }
     float th = 0.0f;
     V3 nn = -norm;
     for (int i = 0; i < 32; i++) {
@@ -217,18 +301,19 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
         const V3 hd = hash33(nn + v3s(fi)) - v3s(0.5f);
         V3 rnd = hd * __builtin_amdgcn_rsqf(dot(hd, hd));
         V3 dir = rnd - (nn * 2.0f) * fminf(0.0f, dot(rnd, nn));  // reflectVector (:70-73)
-        th += sl + dist_probe<SC>(F, pos + dir * sl, cnt);
+        th += sl + dist_at<SC, false>(F, pos + dir * sl, cnt, plane);
     }
     return clamp01(th * 0.03125f);
 }
 
 // output_shader.frag:127-176
 template <int SC>
-__device__ __forceinline__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, Tally& cnt) {
+__device__ __forceinline__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN,
+                                     bool plane, Tally& cnt) {
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     V3 lightDir = normalize(Ld);
-    float occ = ao_real<SC>(F, p, n, cnt);
+    float occ = ao_real<SC>(F, p, n, cnt, plane);
 #ifdef RM_ABLATE_SHADOW
     float sha = 1.0f;
 #else
@@ -243,7 +328,7 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro
 #ifdef RM_ABLATE_SSS
     float th = 0.5f;
 #else
-    float th = thickness<SC>(F, p, n, cnt);
+    float th = thickness<SC>(F, p, n, cnt, plane);
 #endif
     V3 sssl = lightDir + n * 0.6f;
     float sssdot = powf(clamp01(dot(-rd, -sssl)), 1.1f) * 0.3f;
@@ -269,8 +354,9 @@ __device__ __forceinline__ V3 render_reflection(const FrameConst& F, V3 ro, V3 r
     if (dist > 0.0f) {
         Mat m = scene_mat<SC>(F, q);
         V3 p = ro + rd * dist;
-        V3 n = normal_fast<SC>(F, p, cnt);
-        return light_O<SC>(F, m, ro, rd, p, n, n, cnt);
+        const bool pl = plane_probes<SC>(F, p);
+        V3 n = normal_fast<SC>(F, p, cnt, pl);
+        return light_O<SC>(F, m, ro, rd, p, n, n, pl, cnt);
     }
     return background(ro, rd);
 }
@@ -291,10 +377,11 @@ __device__ __forceinline__ V3 render_refraction(const FrameConst& F, V3 ro, V3 r
         }
         Mat m = scene_mat<SC>(F, q);
         V3 p = ro + rd * dist;
-        V3 g = normal_fast<SC>(F, p, cnt);
+        const bool pl = plane_probes<SC>(F, p);
+        V3 g = normal_fast<SC>(F, p, cnt, pl);
         V3 n = g * invert;
         V3 ref = reflect(rd, n);
-        color = color + light_O<SC>(F, m, ro, ref, p, n, g, cnt);
+        color = color + light_O<SC>(F, m, ro, ref, p, n, g, pl, cnt);
         if (invert > 0.0f) break;
         float ior = invert < 0.0f ? m.refraction_index : 1.0f / m.refraction_index;
         V3 raf = refract(rd, n, ior);
@@ -314,8 +401,9 @@ __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally&
     if (!(dist > 0.0f)) return background(ro, rd);
     Mat m = scene_mat<SC>(F, q);
     V3 p = ro + rd * dist;
-    V3 n = normal_fast<SC>(F, p, cnt);
-    V3 color = light_O<SC>(F, m, ro, rd, p, n, n, cnt);
+    const bool pl = plane_probes<SC>(F, p);
+    V3 n = normal_fast<SC>(F, p, cnt, pl);
+    V3 color = light_O<SC>(F, m, ro, rd, p, n, n, pl, cnt);
     float rf = fresnel(m.refraction_index, n, rd, m.transparency > 0.0f ? 0.0f : m.reflectivity);
     if (m.reflectivity > 0.0f) {
         V3 r = reflect(rd, n);
