@@ -58,7 +58,8 @@ def parse():
                     help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
     ap.add_argument("--streams", type=int, default=None, choices=[1, 2],
-                    help="HIP streams frames alternate on (default: 2 for N > 1 over RCCL, else 1)")
+                    help="HIP streams frames alternate on (default 2: frame k+1's waves fill the SIMDs while "
+                         "frame k's longest waves finish; 1 with the gloo rehearsal backend)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "tile16", "tile8"])
     ap.add_argument("--schedule", default="adaptive", choices=["adaptive", "rowmajor"],
                     help="tile dispatch order: costliest tiles of the previous frame first, or row-major")
@@ -265,7 +266,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream)
     chunks = args.chunks if args.chunks is not None else 1
-    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks, streams=args.streams)
+    streams = args.streams or (1 if world > 1 and args.backend == "gloo" else 2)
+    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks, streams=streams)
 
     # instrumented run: ray-steps of this rank's rows, summed over ranks
     r.set_params(count_evals=1)

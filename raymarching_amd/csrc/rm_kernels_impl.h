@@ -10,11 +10,18 @@
 
 namespace rm {
 
+// Minimum waves per SIMD the register allocator must allow.  Scene O asks
+// for 8 (64 VGPRs): its kernel needs ~82, and the few spills to scratch cost
+// less than occupancy 5 does (C5 frame 12.29 -> 11.56 ms,
+// profiles/r02/scene_O_occupancy_ab.jsonl); S0/T fit 8 waves unasked; the
+// glass test scene OG would spill ~80 VGPRs and keeps its allocation.
 #ifndef RM_WAVES_PER_EU
 #define RM_WAVES_PER_EU 1
 #endif
+template <int SC>
+constexpr int kWavesPerEU = SC == SCENE_O ? 8 : RM_WAVES_PER_EU;
 template <int SC, bool COUNT, int K, typename OUT>
-__global__ __launch_bounds__(64 * Tiling<K>::WPB) __attribute__((amdgpu_waves_per_eu(RM_WAVES_PER_EU)))
+__global__ __launch_bounds__(64 * Tiling<K>::WPB) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<SC>)))
 void rm_render_direct(FrameConst F, OUT* __restrict__ out, unsigned long long* __restrict__ evals) {
     render_tile<SC, COUNT, K, OUT>(F, out, evals);
 }

@@ -306,10 +306,12 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
     return clamp01(th * 0.03125f);
 }
 
-// output_shader.frag:127-176
+// output_shader.frag:127-176.  The material of the hit (the SdResult at mq)
+// is evaluated after the AO / shadow / thickness loops and returned in mat: it
+// is not live across them (16 floats fewer in registers during the loops).
 template <int SC>
-__device__ __forceinline__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro, V3 rd, V3 p, V3 n, V3 phongN,
-                                     bool plane, Tally& cnt) {
+__device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, bool plane,
+                                     Mat& mat, Tally& cnt) {
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     V3 lightDir = normalize(Ld);
@@ -319,17 +321,18 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, const Mat& mat, V3 ro
 #else
     float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, length(Ld), cnt);
 #endif
+#ifdef RM_ABLATE_SSS
+    float th = 0.5f;
+#else
+    float th = thickness<SC>(F, p, n, cnt, plane);
+#endif
+    mat = scene_mat<SC>(F, mq);
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     V3 shading =
         phong<SC>(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, p, ro, lightPos, phongN) * shadow_pow<SC>(sha);
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
-#ifdef RM_ABLATE_SSS
-    float th = 0.5f;
-#else
-    float th = thickness<SC>(F, p, n, cnt, plane);
-#endif
     V3 sssl = lightDir + n * 0.6f;
     float sssdot = powf(clamp01(dot(-rd, -sssl)), 1.1f) * 0.3f;
     shading = shading + v3s((sssdot + 0.3f) * th);
@@ -352,11 +355,11 @@ __device__ __forceinline__ V3 render_reflection(const FrameConst& F, V3 ro, V3 r
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
     if (dist > 0.0f) {
-        Mat m = scene_mat<SC>(F, q);
+        Mat m;
         V3 p = ro + rd * dist;
         const bool pl = plane_probes<SC>(F, p);
         V3 n = normal_fast<SC>(F, p, cnt, pl);
-        return light_O<SC>(F, m, ro, rd, p, n, n, pl, cnt);
+        return light_O<SC>(F, q, ro, rd, p, n, n, pl, m, cnt);
     }
     return background(ro, rd);
 }
@@ -375,13 +378,13 @@ __device__ __forceinline__ V3 render_refraction(const FrameConst& F, V3 ro, V3 r
             if (invert > 0.0f) color = color + background(ro, rd);
             break;
         }
-        Mat m = scene_mat<SC>(F, q);
+        Mat m;
         V3 p = ro + rd * dist;
         const bool pl = plane_probes<SC>(F, p);
         V3 g = normal_fast<SC>(F, p, cnt, pl);
         V3 n = g * invert;
         V3 ref = reflect(rd, n);
-        color = color + light_O<SC>(F, m, ro, ref, p, n, g, pl, cnt);
+        color = color + light_O<SC>(F, q, ro, ref, p, n, g, pl, m, cnt);
         if (invert > 0.0f) break;
         float ior = invert < 0.0f ? m.refraction_index : 1.0f / m.refraction_index;
         V3 raf = refract(rd, n, ior);
@@ -399,11 +402,11 @@ __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally&
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
     if (!(dist > 0.0f)) return background(ro, rd);
-    Mat m = scene_mat<SC>(F, q);
+    Mat m;
     V3 p = ro + rd * dist;
     const bool pl = plane_probes<SC>(F, p);
     V3 n = normal_fast<SC>(F, p, cnt, pl);
-    V3 color = light_O<SC>(F, m, ro, rd, p, n, n, pl, cnt);
+    V3 color = light_O<SC>(F, q, ro, rd, p, n, n, pl, m, cnt);
     float rf = fresnel(m.refraction_index, n, rd, m.transparency > 0.0f ? 0.0f : m.reflectivity);
     if (m.reflectivity > 0.0f) {
         V3 r = reflect(rd, n);
