@@ -58,8 +58,9 @@ def parse():
                     help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
     ap.add_argument("--streams", type=int, default=None, choices=[1, 2],
-                    help="HIP streams frames alternate on (default 2: frame k+1's waves fill the SIMDs while "
-                         "frame k's longest waves finish; 1 with the gloo rehearsal backend)")
+                    help="HIP streams frames alternate on (default: 2 for N > 1 over RCCL, else 1; at N = 1 "
+                         "two streams measure ~2 %% faster frames for C3, but each launch then overlaps the next "
+                         "and rocprofv3's per-launch durations no longer equal the kernel's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "tile16", "tile8"])
     ap.add_argument("--schedule", default="adaptive", choices=["adaptive", "rowmajor"],
                     help="tile dispatch order: costliest tiles of the previous frame first, or row-major")
@@ -266,8 +267,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     r.set_stream(stream)
     chunks = args.chunks if args.chunks is not None else 1
-    streams = args.streams or (1 if world > 1 and args.backend == "gloo" else 2)
-    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks, streams=streams)
+    fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks, streams=args.streams)
 
     # instrumented run: ray-steps of this rank's rows, summed over ranks
     r.set_params(count_evals=1)

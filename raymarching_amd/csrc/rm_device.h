@@ -488,12 +488,17 @@ __device__ __forceinline__ float tonemap1(float c, float e2) {
     }
     return col * 0.5f + 0.5f * col * col * (3.0f - 2.0f * col);
 }
-// tonemap -> contrast (common.frag:1067) -> vignette(.., 0.1) (:1072)
+// vignette(.., 0.1)'s factor (common.frag:1072): computed before the render, so
+// one value instead of the two texture coordinates stays live through it
 template <bool FAST>
-__device__ __forceinline__ V3 post_colour(V3 c, float tcx, float tcy) {
+__device__ __forceinline__ float vignette(float tcx, float tcy) {
+    return 0.5f + 0.5f * gpow<FAST>(16.0f * tcx * tcy * (1.0f - tcx) * (1.0f - tcy), 0.1f);
+}
+// tonemap -> contrast (common.frag:1067) -> vignette (v = vignette(texcoord))
+template <bool FAST>
+__device__ __forceinline__ V3 post_colour(V3 c, float v) {
     V3 t = v3(tonemap1<FAST>(c.x, 0.85f), tonemap1<FAST>(c.y, 0.97f), tonemap1<FAST>(c.z, 1.0f));
     t = v3(smoothstep(0.15f, 1.1f, t.x), smoothstep(0.15f, 1.1f, t.y), smoothstep(0.15f, 1.1f, t.z));
-    float v = 0.5f + 0.5f * gpow<FAST>(16.0f * tcx * tcy * (1.0f - tcx) * (1.0f - tcy), 0.1f);
     return t * v;
 }
 

@@ -38,7 +38,8 @@ extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst
         float tcx, tcy;
         V3 ro, rd;
         camera_ray(F, x, y, tcx, tcy, ro, rd);
-        V3 c = post_colour<false>(render_pixel<SCENE_PLUGIN>(F, ro, rd, cnt), tcx, tcy);
+        const float vig = vignette<false>(tcx, tcy);
+        V3 c = post_colour<false>(render_pixel<SCENE_PLUGIN>(F, ro, rd, cnt), vig);
         const size_t i = (size_t)j * F.W + x;
         if (rgba8) static_cast<uint32_t*>(out)[i] = pack_rgba8(c.x, c.y, c.z, 1.0f);
         else static_cast<float4*>(out)[i] = make_float4(c.x, c.y, c.z, 1.0f);

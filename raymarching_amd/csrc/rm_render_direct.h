@@ -55,7 +55,9 @@ __device__ __forceinline__ V3 mnormalize(V3 a) {
 // plane-only when the slack there is >= 2.05.
 template <int SC>
 constexpr bool kPlaneSpans = SC == SCENE_O || SC == SCENE_OG;
-__device__ __forceinline__ float plane_rate(V3 d) { return 1.0f / (1.01f + fabsf(d.y)); }
+__device__ __forceinline__ float plane_rate(V3 d) {  // (v_rcp: 1 ulp is far inside the margin)
+    return __builtin_amdgcn_rcpf(1.01f + fabsf(d.y));
+}
 template <int SC>
 __device__ __forceinline__ bool plane_probes(const FrameConst& F, V3 p) {
     if constexpr (kPlaneSpans<SC>) {
@@ -554,8 +556,9 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
         float tcx, tcy;
         V3 ro, rd;
         camera_ray(F, x, y, tcx, tcy, ro, rd);
+        const float vig = vignette<FastMath<SC>::value>(tcx, tcy);
         V3 c = render_pixel<SC>(F, ro, rd, cnt);
-        c = post_colour<FastMath<SC>::value>(c, tcx, tcy);
+        c = post_colour<FastMath<SC>::value>(c, vig);
         if constexpr (sizeof(OUT) == 4) out[(size_t)j * F.W + x] = pack_rgba8(c.x, c.y, c.z, 1.0f);
         else out[(size_t)j * F.W + x] = make_float4(c.x, c.y, c.z, 1.0f);
     }
