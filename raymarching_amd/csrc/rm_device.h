@@ -222,9 +222,11 @@ __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool 
         }
         float med = __builtin_amdgcn_fmed3f(rx, ry, rz);
         float c = EXACT ? div_const(med - 1.0f, S3[m], INV[m]) : fmaf(med, INV[m], -INV[m]);
-        // if (c > d) d = c;  as one v_max: c and d are NaN together or not at all
-        // (C4 share -2 %, C2 at P1 -2.5 % against compare + select)
-        d = fmaxf(c, d);
+        // if (c > d) d = c;  as one max: c and d are NaN together or not at all
+        // (C4 share -2 %, C2 at P1 -2.5 % against compare + select).  IEEE
+        // maximum (v_maximum3_f32) rather than maxNum: fmaxf's operands get a
+        // canonicalizing v_max(d, d) each fold, maximum's need none.
+        d = __builtin_elementwise_maximum(c, d);
     }
     return d;
 }

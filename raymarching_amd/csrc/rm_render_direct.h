@@ -179,8 +179,8 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
         float D = it == 1 ? t : fmaf(t, P, -h2);
-        float cn = h2 * Q, cd = D * D;
-        bool upd = (D > 0.0f) & (Q >= 0.0f) & (cn * den < num * cd);
+        float cn = h2 * Q, cd = D * fabsf(D);  // D <= 0: cd <= 0 fails the test (cn, den >= 0)
+        bool upd = (Q >= 0.0f) & (cn * den < num * cd);
         num = upd ? cn : num;
         den = upd ? cd : den;
         P = h + h;
@@ -194,7 +194,8 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // divisions and square roots.  With P = 2 ph the reference's y = h^2/P gives
 //   k sqrt(h^2 - y^2) / (t - y) = k h sqrt(P^2 - h^2) / (t P - h^2),
 // and res^2 / k^2 is kept as num/den, candidates h^2 Q / D^2 compared by
-// cross-products (branch-free selects).  Candidates with t - y <= 0 (k d / 0:
+// cross-products (branch-free selects; D |D| for D^2 makes t - y <= 0 fail the
+// comparison without a test of its own).  Candidates with t - y <= 0 (k d / 0:
 // inf or NaN) or h^2 < y^2 (sqrt NaN) never lower res, as GLSL
 // min(res, x) = x < res ? x : res.  On the first step ph = 1e20 makes y
 // vanish: the candidate is k h / t (Q = 1, D = t below).  The occlusion result
@@ -211,8 +212,8 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
         float D = it == 1 ? t : fmaf(t, P, -h2);
-        float cn = h2 * Q, cd = D * D;
-        bool upd = (D > 0.0f) & (Q >= 0.0f) & (cn * den < num * cd);
+        float cn = h2 * Q, cd = D * fabsf(D);  // D <= 0: cd <= 0 fails the test (cn, den >= 0)
+        bool upd = (Q >= 0.0f) & (cn * den < num * cd);
         num = upd ? cn : num;
         den = upd ? cd : den;
         P = h + h;
