@@ -219,10 +219,14 @@ bool compile(const std::string& src, const std::string& file, Code& code, std::s
         log = std::string("hiprtcCreateProgram: ") + hiprtcGetErrorString(r);
         return false;
     }
-    // the flags of scene O's translation unit (raymarching_amd/Makefile)
+    // the flags of scene O's translation unit (raymarching_amd/Makefile), and
+    // the render kernel's occupancy (RM_PLUGIN_WAVES_PER_EU overrides it)
+    const char* env_w = std::getenv("RM_PLUGIN_WAVES_PER_EU");
+    const std::string waves = std::string("-DRM_PLUGIN_WAVES_PER_EU=") +
+                              (env_w && std::atoi(env_w) > 0 ? std::to_string(std::atoi(env_w)) : std::string("1"));
     const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                           "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wno-unused-function",
-                          "-Wno-unused-variable"};
+                          "-Wno-unused-variable", waves.c_str()};
     r = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
     size_t ls = 0;
     if (hiprtcGetProgramLogSize(prog, &ls) == HIPRTC_SUCCESS && ls > 1) {

@@ -19,7 +19,12 @@ struct rm::PluginScene<rm::SCENE_PLUGIN> {
 // output_shader.frag's pass over 8x8-pixel one-wave tiles.  One kernel serves
 // every launch: the output format and the instrumentation are run-time
 // arguments (a plugin compiles one pipeline instead of four).
-extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
+// Minimum waves per SIMD for the register allocator (rm_plugin_host.cpp sets
+// it; a scene's pipeline needs ~150 VGPRs unbounded, occupancy 3).
+#ifndef RM_PLUGIN_WAVES_PER_EU
+#define RM_PLUGIN_WAVES_PER_EU 1
+#endif
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_PLUGIN_WAVES_PER_EU))) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
                                                                   unsigned long long* evals) {
     using namespace rm;
     const uint64_t t_start = F.tile_cost ? clock64() : 0;

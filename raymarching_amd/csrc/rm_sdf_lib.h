@@ -105,8 +105,20 @@ __device__ __forceinline__ vec2& operator*=(vec2& a, float s) { return a = a * s
 // GLSL 1.30 built-ins (min/max/clamp by their spec definitions, mod = x - y floor(x/y))
 __device__ __forceinline__ float abs(float x) { return fabsf(x); }
 __device__ __forceinline__ float sign(float x) { return x > 0.0f ? 1.0f : x < 0.0f ? -1.0f : 0.0f; }
-__device__ __forceinline__ float min(float x, float y) { return y < x ? y : x; }
-__device__ __forceinline__ float max(float x, float y) { return x < y ? y : x; }
+// min / max as single instructions (v_minimum3_f32 / v_maximum3_f32): equal to
+// the GLSL 1.30 definitions (y < x ? y : x, x < y ? y : x) for every non-NaN
+// operand pair up to the sign of a zero result; a NaN operand gives NaN (the
+// definitions return x).  The compare + select pair of the definitions was
+// ~15 % of a plugin's march step.
+__device__ __forceinline__ float min(float x, float y) { return __builtin_elementwise_minimum(x, y); }
+__device__ __forceinline__ float max(float x, float y) { return __builtin_elementwise_maximum(x, y); }
+// x / k for a divisor that is a constant once the scene is inlined: one
+// Markstein correction of x * RN(1/k) (rm_device.h div_const), the correctly
+// rounded quotient (checked exhaustively over two binades of x for the
+// library's divisors), 3 VALU instead of the ~12 of the IEEE division.
+__device__ __forceinline__ float div_k(float x, float k) {
+    return __builtin_constant_p(k) ? div_const(x, k, 1.0f / k) : x / k;
+}
 __device__ __forceinline__ float clamp(float x, float lo, float hi) { return min(max(x, lo), hi); }
 __device__ __forceinline__ float mix(float x, float y, float a) { return x + (y - x) * a; }  // rm_device.h gmix
 __device__ __forceinline__ float mod(float x, float y) { return x - y * floorf(x / y); }
@@ -239,7 +251,8 @@ __device__ __forceinline__ SdResult sdUnion(const SdResult& a, const SdResult& b
 // common.frag:72-85: k.x blends the shape, k.y the material
 __device__ __forceinline__ SdResult sminCubic(const SdResult& a, const SdResult& b, vec2 k) {
     k = max(k, 0.0001f);
-    vec2 h = max(k - fabsf(a.dist - b.dist), 0.0f) / k;
+    const vec2 x = max(k - fabsf(a.dist - b.dist), 0.0f);
+    vec2 h = vec2(div_k(x.x, k.x), div_k(x.y, k.y));
     vec2 m = h * h * h * 0.5f;
     vec2 s = m * k * (1.0f / 3.0f);
     SdResult res;
@@ -259,28 +272,28 @@ __device__ __forceinline__ float opUnion(float d1, float d2) { return min(d1, d2
 __device__ __forceinline__ float opSubtraction(float d1, float d2) { return max(-d1, d2); }
 __device__ __forceinline__ float opIntersection(float d1, float d2) { return max(d1, d2); }
 __device__ __forceinline__ float opSmoothUnion(float d1, float d2, float k) {
-    float h = clamp(0.5f + 0.5f * (d2 - d1) / k, 0.0f, 1.0f);
+    float h = clamp(0.5f + div_k(0.5f * (d2 - d1), k), 0.0f, 1.0f);
     return mix(d2, d1, h) - k * h * (1.0f - h);
 }
 __device__ __forceinline__ float opSmoothSubtraction(float d1, float d2, float k) {
-    float h = clamp(0.5f - 0.5f * (d2 + d1) / k, 0.0f, 1.0f);
+    float h = clamp(0.5f - div_k(0.5f * (d2 + d1), k), 0.0f, 1.0f);
     return mix(d2, -d1, h) + k * h * (1.0f - h);
 }
 __device__ __forceinline__ float opSmoothIntersection(float d1, float d2, float k) {
-    float h = clamp(0.5f - 0.5f * (d2 - d1) / k, 0.0f, 1.0f);
+    float h = clamp(0.5f - div_k(0.5f * (d2 - d1), k), 0.0f, 1.0f);
     return mix(d2, d1, h) + k * h * (1.0f - h);
 }
 // common.frag:128-131
 __device__ __forceinline__ float sdf_blend(float d1, float d2, float a) { return a * d1 + (1.0f - a) * d2; }
 // common.frag:135-139
 __device__ __forceinline__ float smin(float a, float b, float k) {
-    float h = clamp(0.5f + 0.5f * (b - a) / k, 0.0f, 1.0f);
+    float h = clamp(0.5f + div_k(0.5f * (b - a), k), 0.0f, 1.0f);
     return mix(b, a, h) - k * h * (1.0f - h);
 }
 // common.frag:142-146
 __device__ __forceinline__ float smin_exp(float a, float b, float k = 32.0f) {
     float res = exp(-k * a) + exp(-k * b);
-    return -log(max(0.0001f, res)) / k;
+    return div_k(-log(max(0.0001f, res)), k);
 }
 // common.frag:148-151
 __device__ __forceinline__ float rounding(float d, float h = 0.1f) { return d - h; }
@@ -334,88 +347,106 @@ __device__ __forceinline__ mat4 scale_inv(vec3 scale) {
                 vec4(0, 0, 0, 1));
 }
 
+// Row vectors times the structured matrices above, rounded as the full
+// vec4 * mat4 product rounds them: a product with an exact 0 or 1 entry is an
+// exact zero or the operand itself, and adding an exact zero leaves a sum
+// unchanged for finite operands (up to the sign of a zero result), so only the
+// other terms are formed, in the dot product's order.  (IEEE semantics keep
+// the compiler from dropping x * 0 itself: it is NaN for an infinite x.)
+struct Rot {
+    float c, s;
+};
+__device__ __forceinline__ Rot rot_of(float angle_deg) {  // cos / sin as rotationX/Y/Z form them
+    float a = radians(angle_deg);
+    return Rot{cos(a), sin(a)};
+}
+__device__ __forceinline__ vec4 mul_rx(vec4 v, Rot r) {  // v * rotationX
+    return vec4(v.x, v.y * r.c + v.z * -r.s, v.y * r.s + v.z * r.c, v.w);
+}
+__device__ __forceinline__ vec4 mul_ry(vec4 v, Rot r) {  // v * rotationY
+    return vec4(v.x * r.c + v.z * r.s, v.y, v.x * -r.s + v.z * r.c, v.w);
+}
+__device__ __forceinline__ vec4 mul_rz(vec4 v, Rot r) {  // v * rotationZ
+    return vec4(v.x * r.c + v.y * -r.s, v.x * r.s + v.y * r.c, v.z, v.w);
+}
+__device__ __forceinline__ vec4 mul_t(vec4 v, vec3 pos) {  // v * translation_inv(pos)
+    return vec4(v.x + v.w * -pos.x, v.y + v.w * -pos.y, v.z + v.w * -pos.z, v.w);
+}
+__device__ __forceinline__ vec4 mul_s(vec4 v, vec3 scale) {  // v * scale_inv(scale)
+    return vec4(v.x * (1.0f / scale.x), v.y * (1.0f / scale.y), v.z * (1.0f / scale.z), v.w);
+}
+__device__ __forceinline__ vec4 mul_yxz(vec4 v, vec3 rot) {  // v * r_y * r_x * r_z
+    return mul_rz(mul_rx(mul_ry(v, rot_of(-rot.y)), rot_of(-rot.x)), rot_of(-rot.z));
+}
+
 // common.frag:248-267
 __device__ __forceinline__ vec3 transform(vec3 sp, vec3 pos, vec3 rot, vec3 scale) {
-    mat4 s = scale_inv(scale), r_y = rotationY(-rot.y), r_x = rotationX(-rot.x), r_z = rotationZ(-rot.z);
-    mat4 t = translation_inv(pos);
-    return xyz(vec4(sp, 1.0f) * t * r_y * r_x * r_z * s);
+    return xyz(mul_s(mul_yxz(mul_t(vec4(sp, 1.0f), pos), rot), scale));
 }
 // common.frag:269-282
 __device__ __forceinline__ vec3 transformTR(vec3 sp, vec3 pos, vec3 rot) {
-    mat4 r_y = rotationY(-rot.y), r_x = rotationX(-rot.x), r_z = rotationZ(-rot.z), t = translation_inv(pos);
-    return xyz(vec4(sp, 1.0f) * t * r_y * r_x * r_z);
+    return xyz(mul_yxz(mul_t(vec4(sp, 1.0f), pos), rot));
 }
 // common.frag:284-321
 __device__ __forceinline__ vec3 transformTRX(vec3 sp, vec3 pos, float rot_x) {
-    return xyz(vec4(sp, 1.0f) * translation_inv(pos) * rotationX(-rot_x));
+    return xyz(mul_rx(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_x)));
 }
 __device__ __forceinline__ vec3 transformTRY(vec3 sp, vec3 pos, float rot_y) {
-    return xyz(vec4(sp, 1.0f) * translation_inv(pos) * rotationY(-rot_y));
+    return xyz(mul_ry(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_y)));
 }
 __device__ __forceinline__ vec3 transformTRZ(vec3 sp, vec3 pos, float rot_z) {
-    return xyz(vec4(sp, 1.0f) * translation_inv(pos) * rotationZ(-rot_z));
+    return xyz(mul_rz(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_z)));
 }
 // common.frag:323-378
 __device__ __forceinline__ vec3 transformTRXS(vec3 sp, vec3 pos, float rot_x, vec3 scale) {
-    mat4 s = scale_inv(scale), r_x = rotationX(-rot_x), t = translation_inv(pos);
-    return xyz(vec4(sp, 1.0f) * t * r_x * s);
+    return xyz(mul_s(mul_rx(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_x)), scale));
 }
 __device__ __forceinline__ vec3 transformTRYS(vec3 sp, vec3 pos, float rot_y, vec3 scale) {
-    mat4 s = scale_inv(scale), r_y = rotationY(-rot_y), t = translation_inv(pos);
-    return xyz(vec4(sp, 1.0f) * t * r_y * s);
+    return xyz(mul_s(mul_ry(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_y)), scale));
 }
 __device__ __forceinline__ vec3 transformTRZS(vec3 sp, vec3 pos, float rot_z, vec3 scale) {
-    mat4 s = scale_inv(scale), r_z = rotationZ(-rot_z), t = translation_inv(pos);
-    return xyz(vec4(sp, 1.0f) * t * r_z * s);
+    return xyz(mul_s(mul_rz(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_z)), scale));
 }
 // common.frag:380-432
 __device__ __forceinline__ vec3 transformTRS1(vec3 sp, vec3 pos, vec3 rot, float scale) {
-    mat4 r_y = rotationY(-rot.y), r_x = rotationX(-rot.x), r_z = rotationZ(-rot.z), t = translation_inv(pos);
-    return xyz(vec4(sp, 1.0f) * t * r_y * r_x * r_z) / scale;
+    return xyz(mul_yxz(mul_t(vec4(sp, 1.0f), pos), rot)) / scale;
 }
 __device__ __forceinline__ vec3 transformTRXS1(vec3 sp, vec3 pos, float rot_x, float scale) {
-    return xyz(vec4(sp, 1.0f) * translation_inv(pos) * rotationX(-rot_x)) / scale;
+    return xyz(mul_rx(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_x))) / scale;
 }
 __device__ __forceinline__ vec3 transformTRYS1(vec3 sp, vec3 pos, float rot_y, float scale) {
-    return xyz(vec4(sp, 1.0f) * translation_inv(pos) * rotationY(-rot_y)) / scale;
+    return xyz(mul_ry(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_y))) / scale;
 }
 __device__ __forceinline__ vec3 transformTRZS1(vec3 sp, vec3 pos, float rot_z, float scale) {
-    return xyz(vec4(sp, 1.0f) * translation_inv(pos) * rotationZ(-rot_z)) / scale;
+    return xyz(mul_rz(mul_t(vec4(sp, 1.0f), pos), rot_of(-rot_z))) / scale;
 }
 // common.frag:434-462
-__device__ __forceinline__ vec3 transformR(vec3 sp, vec3 rot) {
-    mat4 r_y = rotationY(-rot.y), r_x = rotationX(-rot.x), r_z = rotationZ(-rot.z);
-    return xyz(vec4(sp, 1.0f) * r_y * r_x * r_z);
-}
-__device__ __forceinline__ vec3 transformRX(vec3 sp, float rot_x) { return xyz(vec4(sp, 1.0f) * rotationX(-rot_x)); }
-__device__ __forceinline__ vec3 transformRY(vec3 sp, float rot_y) { return xyz(vec4(sp, 1.0f) * rotationY(-rot_y)); }
-__device__ __forceinline__ vec3 transformRZ(vec3 sp, float rot_z) { return xyz(vec4(sp, 1.0f) * rotationZ(-rot_z)); }
+__device__ __forceinline__ vec3 transformR(vec3 sp, vec3 rot) { return xyz(mul_yxz(vec4(sp, 1.0f), rot)); }
+__device__ __forceinline__ vec3 transformRX(vec3 sp, float rot_x) { return xyz(mul_rx(vec4(sp, 1.0f), rot_of(-rot_x))); }
+__device__ __forceinline__ vec3 transformRY(vec3 sp, float rot_y) { return xyz(mul_ry(vec4(sp, 1.0f), rot_of(-rot_y))); }
+__device__ __forceinline__ vec3 transformRZ(vec3 sp, float rot_z) { return xyz(mul_rz(vec4(sp, 1.0f), rot_of(-rot_z))); }
 // common.frag:464-501
 __device__ __forceinline__ vec3 transformRXS(vec3 sp, float rot_x, vec3 scale) {
-    mat4 s = scale_inv(scale), r_x = rotationX(-rot_x);
-    return xyz(vec4(sp, 1.0f) * r_x * s);
+    return xyz(mul_s(mul_rx(vec4(sp, 1.0f), rot_of(-rot_x)), scale));
 }
 __device__ __forceinline__ vec3 transformRYS(vec3 sp, float rot_y, vec3 scale) {
-    mat4 s = scale_inv(scale), r_y = rotationY(-rot_y);
-    return xyz(vec4(sp, 1.0f) * r_y * s);
+    return xyz(mul_s(mul_ry(vec4(sp, 1.0f), rot_of(-rot_y)), scale));
 }
 __device__ __forceinline__ vec3 transformRZS(vec3 sp, float rot_z, vec3 scale) {
-    mat4 s = scale_inv(scale), r_z = rotationZ(-rot_z);
-    return xyz(vec4(sp, 1.0f) * r_z * s);
+    return xyz(mul_s(mul_rz(vec4(sp, 1.0f), rot_of(-rot_z)), scale));
 }
 // common.frag:503-531
 __device__ __forceinline__ vec3 transformRS1(vec3 sp, vec3 rot, float scale) {
-    mat4 r_y = rotationY(-rot.y), r_x = rotationX(-rot.x), r_z = rotationZ(-rot.z);
-    return xyz(vec4(sp, 1.0f) * r_y * r_x * r_z) / scale;
+    return xyz(mul_yxz(vec4(sp, 1.0f), rot)) / scale;
 }
 __device__ __forceinline__ vec3 transformRXS1(vec3 sp, float rot_x, float scale) {
-    return xyz(vec4(sp, 1.0f) * rotationX(-rot_x)) / scale;
+    return xyz(mul_rx(vec4(sp, 1.0f), rot_of(-rot_x))) / scale;
 }
 __device__ __forceinline__ vec3 transformRYS1(vec3 sp, float rot_y, float scale) {
-    return xyz(vec4(sp, 1.0f) * rotationY(-rot_y)) / scale;
+    return xyz(mul_ry(vec4(sp, 1.0f), rot_of(-rot_y))) / scale;
 }
 __device__ __forceinline__ vec3 transformRZS1(vec3 sp, float rot_z, float scale) {
-    return xyz(vec4(sp, 1.0f) * rotationZ(-rot_z)) / scale;
+    return xyz(mul_rz(vec4(sp, 1.0f), rot_of(-rot_z))) / scale;
 }
 
 // --------------------------------------------------- domain operations
@@ -456,10 +487,13 @@ __device__ __forceinline__ float cube(vec4 s, vec3 p) {
     vec3 q = abs(p - xyz(s)) - s.w;
     return length(max(q, 0.0f)) + min(max(q.x, max(q.y, q.z)), 0.0f);
 }
+// = mc exactly: if mc <= 0 every max(di, 0) is 0 and min(mc, 0) = mc;
+// otherwise the rounded sum of squares is >= RN(mc^2), whose correctly rounded
+// square root is mc, so the length is >= mc (a plugin's sqrt is correctly
+// rounded, rm_plugin_host.cpp).  No length, no sqrt.
 __device__ __forceinline__ float sdBox(vec3 p, vec3 b) {
     vec3 di = abs(p) - b;
-    float mc = max(di.x, max(di.y, di.z));
-    return min(mc, length(max(di, 0.0f)));
+    return max(di.x, max(di.y, di.z));
 }
 __device__ __forceinline__ float cylinder(vec3 p, float r) { return length(xy(p)) - r; }
 __device__ __forceinline__ float cone(vec3 p, vec2 c) {  // c must be normalized
@@ -497,13 +531,17 @@ __device__ __forceinline__ vec3 mengersponge(vec3 p) {
     vec3 res = vec3(d, 1.0f, 0.0f);
     float s = 1.0f;
     for (int m = 0; m < 3; m++) {
+        // fold m yields c = (min(da, db, dc) - 1) / s <= 1/s (r <= 2), so once
+        // d >= RN(1/s) no later fold can win `c > d`: an exact early exit
+        // (rm_device.h sponge_folds), which skips the folds far from the sponge
+        if (!(d < 1.0f / (s * 3.0f))) break;
         vec3 a = mod(p * s, 2.0f) - 1.0f;
         s *= 3.0f;
         vec3 r = abs(1.0f - 3.0f * abs(a));
         float da = max(r.x, r.y);
         float db = max(r.y, r.z);
         float dc = max(r.z, r.x);
-        float c = (min(da, min(db, dc)) - 1.0f) / s;
+        float c = div_k(min(da, min(db, dc)) - 1.0f, s);
         if (c > d) {
             d = c;
             res = vec3(d, 0.2f * da * db * dc, (1.0f + (float)m) / 4.0f);
