@@ -10,8 +10,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iterator>
@@ -240,6 +242,17 @@ bool is_device_ptr(const void *p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+// Workgroups at the head of an ordered launch that render scene T with the
+// latency-optimized folds (FrameConst.lat_tiles); RM_LAT_TILES overrides the
+// default (tuning).
+int lat_tiles() {
+    static const int n = [] {
+        const char *e = std::getenv("RM_LAT_TILES");
+        return e ? std::max(0, std::atoi(e)) : 2048;
+    }();
+    return n;
+}
+
 FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int shard, int nrows) {
     FrameConst F;
     std::memset(&F, 0, sizeof(F));
@@ -264,6 +277,7 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int
     F.max_steps = c->params.max_steps;
     // 0 (unbounded, the reference) travels as INT_MAX: one compare per shadow step
     F.shadow_max_steps = c->params.shadow_max_steps > 0 ? c->params.shadow_max_steps : 0x7fffffff;
+    F.lat_tiles = lat_tiles();
     for (int i = 0; i < 32; i++) {
         F.hash11[i] = hash11((float)i);
         F.sss_floor[0][i] = sss_floor_term(1.0f, i);

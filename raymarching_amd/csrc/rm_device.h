@@ -56,6 +56,8 @@ struct FrameConst {
     uint32_t* evals_map;           // instrumented launches: sceneSDF calls per pixel (packed rows), or null
     const uint32_t* tile_order;    // workgroup i renders tile tile_order[i] (a permutation), or null: tile i
     uint32_t* tile_cost;           // if set: each one-wave tile's duration in shader clocks (adaptive order)
+    int lat_tiles;                 // with tile_order: the first lat_tiles workgroups (the costliest tiles) render
+                                   // with the latency-optimized Menger folds (scene T, render_tile)
 };
 
 // Buckets of the adaptive dispatch order (rm_capi.cpp, rm_kernels.hip): 256
@@ -192,14 +194,19 @@ __device__ __forceinline__ float sponge_box(V3 p) {
 // shadow steps) whole waves skip the folds.  (Wave-uniform variants of this
 // branch and of the march loops, __ballot-driven with lanes frozen by
 // selects, measured 1.13 ms against 0.93 ms per 4096^2 T frame: DESIGN.md.)
-template <bool EXACT>
+// NB: how many of the three folds keep their exit test.  A fold computed past
+// its exit point leaves d unchanged, so any NB gives the same distance: 3 (the
+// default) executes the fewest instructions, 1 the fewest branches and exec-mask
+// updates, which is what bounds the latency of a lone long wave (the tail of a
+// launch: render_tile's latency tiles).
+template <bool EXACT, int NB = 3>
 __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool active = true) {
     constexpr float SH[3] = {0.5f, 1.5f, 4.5f};                      // s/2 before s *= 3
     constexpr float S3[3] = {3.0f, 9.0f, 27.0f};                     // s after s *= 3
     constexpr float INV[3] = {1.0f / 3.0f, 1.0f / 9.0f, 1.0f / 27.0f};
 #pragma unroll
     for (int m = 0; m < 3; m++) {
-        if (!(active && d < INV[m])) return d;
+        if (m < NB && !(active && d < INV[m])) return d;
         fl += FL_FOLD;
         float rx, ry, rz;
         if constexpr (EXACT) {
@@ -230,9 +237,9 @@ __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool 
     }
     return d;
 }
-template <bool EXACT>
+template <bool EXACT, int NB = 3>
 __device__ __forceinline__ float menger(V3 p, uint32_t& fl, bool active = true) {
-    return sponge_folds<EXACT>(p, sponge_box(p), fl, active);
+    return sponge_folds<EXACT, NB>(p, sponge_box(p), fl, active);
 }
 
 // transformR(p - vec3(0,3,0), vec3(180, 2t, 0)): row vector times rotationY
@@ -272,12 +279,13 @@ __device__ __forceinline__ V3 at(const LinRay& r, float t) {
 // scene T's sceneSDF at depth t of a sponge-space ray: one ray-step on the
 // active lanes (inactive lanes compute a value nobody reads, without forcing
 // folds on the wave)
+template <int NB = 3>
 __device__ __forceinline__ float menger_at(const LinRay& r, float t, Tally& n, bool active = true) {
     if (active) {
         n.evals++;
         n.flop += FL_LINRAY + FL_BOX;
     }
-    return menger<false>(at(r, t), n.flop, active);
+    return menger<false, NB>(at(r, t), n.flop, active);
 }
 
 // sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4
@@ -373,7 +381,7 @@ __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n) {
 // Scene distances ("one ray-step" = one call).  EXACT keeps the GLSL's
 // roundings (scene O's marches and normals, whose results feed the normal
 // hash); the fast form serves every other call.
-template <int SC, bool EXACT>
+template <int SC, bool EXACT, int NB = 3>
 __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p, Tally& n) {
     if constexpr (SC == SCENE_S0) {
         n.evals++;
@@ -382,7 +390,7 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p, Tally& n)
     } else if constexpr (SC == SCENE_T) {
         n.evals++;
         n.flop += FL_TRANSFORM + FL_BOX;
-        return menger<EXACT>(sponge_space<EXACT>(F, p), n.flop);  // template.frag:41 (repaired)
+        return menger<EXACT, NB>(sponge_space<EXACT>(F, p), n.flop);  // template.frag:41 (repaired)
     } else if constexpr (SC == SCENE_PLUGIN) {
         n.evals++;
         n.flop += PluginScene<SC>::flop;

@@ -34,13 +34,13 @@ __device__ __forceinline__ float mpow(float x, float y) {
 }
 // the scene distance for marches and normals (exact for scene O), and for
 // the AO / shadow / thickness probes, whose results are smooth in the distance
-template <int SC>
+template <int SC, int NB = 3>
 __device__ __forceinline__ float dist_march(const FrameConst& F, V3 p, Tally& cnt) {
-    return scene_dist<SC, !FastMath<SC>::value>(F, p, cnt);
+    return scene_dist<SC, !FastMath<SC>::value, NB>(F, p, cnt);
 }
-template <int SC>
+template <int SC, int NB = 3>
 __device__ __forceinline__ float dist_probe(const FrameConst& F, V3 p, Tally& cnt) {
-    return scene_dist<SC, false>(F, p, cnt);
+    return scene_dist<SC, false, NB>(F, p, cnt);
 }
 template <int SC>
 __device__ __forceinline__ V3 mnormalize(V3 a) {
@@ -71,7 +71,7 @@ __device__ __forceinline__ bool plane_probes(const FrameConst& F, V3 p) {
     }
 }
 // a probe's distance: EXACT = the march form (normals), else the probe form
-template <int SC, bool EXACT>
+template <int SC, bool EXACT, int NB = 3>
 __device__ __forceinline__ float dist_at(const FrameConst& F, V3 p, Tally& cnt, bool plane) {
     if constexpr (kPlaneSpans<SC>) {
         if (plane) {
@@ -79,18 +79,18 @@ __device__ __forceinline__ float dist_at(const FrameConst& F, V3 p, Tally& cnt, 
             return p.y;
         }
     }
-    if constexpr (EXACT) return dist_march<SC>(F, p, cnt);
-    else return dist_probe<SC>(F, p, cnt);
+    if constexpr (EXACT) return dist_march<SC, NB>(F, p, cnt);
+    else return dist_probe<SC, NB>(F, p, cnt);
 }
 
 // common.frag:697-708 (tetrahedral gradient, h = 0.001)
-template <int SC>
+template <int SC, int NB = 3>
 __device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt, bool plane = false) {
     const float h = 0.001f;
-    float d0 = dist_at<SC, true>(F, p + v3(h, -h, -h), cnt, plane);
-    float d1 = dist_at<SC, true>(F, p + v3(-h, -h, h), cnt, plane);
-    float d2 = dist_at<SC, true>(F, p + v3(-h, h, -h), cnt, plane);
-    float d3 = dist_at<SC, true>(F, p + v3(h, h, h), cnt, plane);
+    float d0 = dist_at<SC, true, NB>(F, p + v3(h, -h, -h), cnt, plane);
+    float d1 = dist_at<SC, true, NB>(F, p + v3(-h, -h, h), cnt, plane);
+    float d2 = dist_at<SC, true, NB>(F, p + v3(-h, h, -h), cnt, plane);
+    float d3 = dist_at<SC, true, NB>(F, p + v3(h, h, h), cnt, plane);
     V3 g = v3(d0, -d0, -d0) + v3(-d1, -d1, d1);
     g = g + v3(-d2, d2, -d2);
     g = g + v3(d3, d3, d3);
@@ -201,6 +201,7 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // vanish: the candidate is k h / t (Q = 1, D = t below).  The occlusion result
 // is recovered after the loop from the last h (a lane leaves through
 // t >= maxt only with h >= 0.001).
+template <int NB = 3>
 __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                 Tally& cnt) {
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
@@ -208,7 +209,7 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
     // one exit test per step (occluded, t >= maxt, or the optional step cap);
     // t grows by >= 0.001 per continuing step, NaN leaves
     for (int it = 1; it == 1 ? t < maxt : true; it++) {
-        h = menger_at(s, t, cnt);
+        h = menger_at<NB>(s, t, cnt);
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
         float D = it == 1 ? t : fmaf(t, P, -h2);
@@ -227,10 +228,11 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
 // depth of the point the reference returns (ZFAR on escape).  depth < ZFAR
 // holds at a hit and after step exhaustion, so the escape value is set once,
 // after the loop.
+template <int NB = 3>
 __device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s, Tally& cnt) {
     float depth = ZNEAR;
     for (int i = 0; i < F.max_steps; i++) {
-        float dist = menger_at(s, depth, cnt);
+        float dist = menger_at<NB>(s, depth, cnt);
         bool hit = dist < 0.001f;
         depth = hit ? depth : depth + dist;
         if (hit | (depth >= ZFAR)) break;  // one exit test per step
@@ -239,13 +241,13 @@ __device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s
 }
 
 // common.frag:850-866
-template <int SC>
+template <int SC, int NB = 3>
 __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tally& cnt, bool plane = false) {
     float sum = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         V3 p = pos + (n * (float)(i + 1)) * 0.2f;
-        sum += (1.0f / (float)(1 << i)) * dist_at<SC, false>(F, p, cnt, plane);
+        sum += (1.0f / (float)(1 << i)) * dist_at<SC, false, NB>(F, p, cnt, plane);
     }
     // maxSum = sum_i 2^-i (i+1) 0.2, accumulated in f32 as the reference does
     float maxSum = 0.0f;
@@ -425,22 +427,23 @@ __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally&
     return color;
 }
 
-// template.frag:45-76 (scene T)
+// template.frag:45-76 (scene T); NB: sponge_folds
+template <int NB = 3>
 __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     constexpr int SC = SCENE_T;
-    V3 p = ro + rd * cast_ray_T(F, sponge_ray(F, ro, rd), cnt);
-    V3 n = normal_fast<SC>(F, p, cnt);
+    V3 p = ro + rd * cast_ray_T<NB>(F, sponge_ray(F, ro, rd), cnt);
+    V3 n = normal_fast<SC, NB>(F, p, cnt);
     // getColorReflect (common.frag:991-1002); its dead nr normal is skipped
     V3 rdir = reflect(rd, n);
     V3 ror = p + rdir * 0.01f;
-    V3 pr = ror + rdir * cast_ray_T(F, sponge_ray(F, ror, rdir), cnt);
+    V3 pr = ror + rdir * cast_ray_T<NB>(F, sponge_ray(F, ror, rdir), cnt);
     float c = clamp01(length(pr - p) * (1.0f / 3.0f));
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     float ld2 = dot(Ld, Ld);
     V3 lightDir = Ld * __builtin_amdgcn_rsqf(ld2);
-    float occ = ao_real<SC>(F, p, n, cnt);
-    float sha = soft_shadow2_T(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
+    float occ = ao_real<SC, NB>(F, p, n, cnt);
+    float sha = soft_shadow2_T<NB>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     float fre = clamp01(1.0f + dot(n, rd));
@@ -495,10 +498,10 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-template <int SC>
+template <int SC, int NB = 3>
 __device__ __forceinline__ V3 render_pixel(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     if constexpr (SC == SCENE_S0) return render_S0(F, ro, rd, cnt);
-    else if constexpr (SC == SCENE_T) return render_T(F, ro, rd, cnt);
+    else if constexpr (SC == SCENE_T) return render_T<NB>(F, ro, rd, cnt);
     else return render_O<SC>(F, ro, rd, cnt);  // O, OG and plugins: output_shader.frag's render()
 }
 
@@ -544,6 +547,11 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
     const uint64_t t_start = T::WPB == 1 && F.tile_cost ? clock64() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int bx = blockIdx.x, by = blockIdx.y;
+    // scene T: the first lat_tiles workgroups of an ordered launch are its
+    // costliest tiles, whose lone waves end the launch; they render with one
+    // fold exit test instead of three (fewer branches, more VALU: C4 share and
+    // C2 tails -16..19 %, a whole C3 frame +5 % if every tile did)
+    const bool lat = T::WPB == 1 && SC == SCENE_T && F.tile_order && (int)(by * gridDim.x + bx) < F.lat_tiles;
     if (F.tile_order) {  // dispatch order != tile order (costliest tiles first, rm_set_tile_order)
         const uint32_t t = F.tile_order[by * gridDim.x + bx];
         bx = t % gridDim.x;
@@ -558,7 +566,14 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
         V3 ro, rd;
         camera_ray(F, x, y, tcx, tcy, ro, rd);
         const float vig = vignette<FastMath<SC>::value>(tcx, tcy);
-        V3 c = render_pixel<SC>(F, ro, rd, cnt);
+        V3 c;
+        if constexpr (SC == SCENE_T) {
+            if (lat) c = render_pixel<SC, 1>(F, ro, rd, cnt);
+            else c = render_pixel<SC>(F, ro, rd, cnt);
+        } else {
+            (void)lat;
+            c = render_pixel<SC>(F, ro, rd, cnt);
+        }
         c = post_colour<FastMath<SC>::value>(c, vig);
         if constexpr (sizeof(OUT) == 4) out[(size_t)j * F.W + x] = pack_rgba8(c.x, c.y, c.z, 1.0f);
         else out[(size_t)j * F.W + x] = make_float4(c.x, c.y, c.z, 1.0f);
