@@ -340,7 +340,10 @@ __device__ __forceinline__ void tap2(const LevelF& A, const LevelF& B, const Axi
 // depend on x or y alone, so the 10 column and 10 row axes are formed once per
 // lane (the general kernel forms them per tap: same values).
 // 5 waves per SIMD (<= 96 VGPRs, a 32-byte spill): hides more scalar-load latency than 4 (-4 %)
-__global__ __launch_bounds__(256, 5) void rm_bloom_min_kernel(Level L0, LevelF A, LevelF B, uint32_t* __restrict__ out,
+#ifndef RM_BLOOM_WAVES
+#define RM_BLOOM_WAVES 5
+#endif
+__global__ __launch_bounds__(256, RM_BLOOM_WAVES) void rm_bloom_min_kernel(Level L0, LevelF A, LevelF B, uint32_t* __restrict__ out,
                                                            int W, int H, float fr) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7), y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
