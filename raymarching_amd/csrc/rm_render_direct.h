@@ -436,14 +436,22 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
     // getColorReflect (common.frag:991-1002); its dead nr normal is skipped
     V3 rdir = reflect(rd, n);
     V3 ror = p + rdir * 0.01f;
+#ifdef RM_ABLATE_REFLECT
+    V3 pr = ror;
+#else
     V3 pr = ror + rdir * cast_ray_T<NB>(F, sponge_ray(F, ror, rdir), cnt);
+#endif
     float c = clamp01(length(pr - p) * (1.0f / 3.0f));
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     float ld2 = dot(Ld, Ld);
     V3 lightDir = Ld * __builtin_amdgcn_rsqf(ld2);
     float occ = ao_real<SC, NB>(F, p, n, cnt);
+#ifdef RM_ABLATE_SHADOW
+    float sha = 1.0f;
+#else
     float sha = soft_shadow2_T<NB>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
+#endif
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     float fre = clamp01(1.0f + dot(n, rd));

@@ -682,3 +682,22 @@ def test_adaptive_dispatch_order_keeps_pixels(R, torch_cuda, scene):
         R.set_tile_order(np.zeros(tx * ty, np.uint32))  # not a permutation
     R.set_tile_order(None)
     R.set_params(schedule=1)
+
+
+def test_latency_tiles_keep_pixels(R, torch_cuda):
+    """Scene T: the first 2048 workgroups of an ordered launch
+    render with one Menger fold exit test instead of three.  A 512x320 frame
+    (2560 tiles) mixes both kinds; every ordered launch writes the row-major
+    frame bit for bit, and the ray-step count is unchanged."""
+    torch = torch_cuda
+    setup(R, "T", POSES["P1"], 128)
+    W, H = 512, 320
+    R.set_params(count_evals=1, schedule=0)
+    ref, st = R.render_rgba8(W, H, stats=True)
+    R.set_params(count_evals=0, schedule=1)
+    for _ in range(4):
+        assert torch.equal(R.render_rgba8(W, H), ref)
+    R.set_params(count_evals=1)
+    a, sa = R.render_rgba8(W, H, stats=True)
+    assert torch.equal(a, ref) and sa["evals"] == st["evals"]
+    R.set_params(count_evals=0)
