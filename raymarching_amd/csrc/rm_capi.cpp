@@ -53,10 +53,12 @@ struct rm_ctx {
     int64_t tile_order_n = 0;
     // adaptive dispatch order (rm_params.schedule): per launch geometry and
     // stream, the tile durations of the last launch and the order they give
-    // Launch k of a geometry writes its tile durations into cost[k & 1]; the
-    // sort of those durations runs on the context's side stream, overlapping
-    // launch k + 1, and writes order[k & 1], which launch k + 2 dispatches
-    // (after waiting for that sort's event).
+    // Every sched_period()-th launch of a geometry (L_s = s * period, s = 0, 1,
+    // ...) writes its tile durations into cost[s & 1]; sort s of those
+    // durations runs on the context's side stream, overlapping the next
+    // launch, and writes order[s & 1], which launches L_s + 2 .. L_{s+1} + 1
+    // dispatch (the first of them waits for the sort's event).  The other
+    // launches write no durations.
     struct Sched {
         uint64_t key = 0;
         hipStream_t stream = nullptr;
@@ -253,6 +255,19 @@ int lat_tiles() {
     return n;
 }
 
+// Launches per dispatch-order sort of a geometry (rm_ctx::Sched): 4 -- an
+// order is at most 5 launches old (frame-to-frame coherence keeps it good), and
+// the duration stores, the sort and the cross-stream events run on one launch
+// in four (C3 frame 0.683 -> 0.672 ms).  RM_SCHED_PERIOD
+// overrides it (1 = re-sort after every launch).
+int sched_period() {
+    static const int n = [] {
+        const char *e = std::getenv("RM_SCHED_PERIOD");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
+    }();
+    return n;
+}
+
 FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int shard, int nrows) {
     FrameConst F;
     std::memset(&F, 0, sizeof(F));
@@ -381,11 +396,12 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         sc = sched_slot(ctx, W, H, band, nshards, shard, row0, count, st);
         if (st != RM_OK) return st;
         if (sc) {
-            const size_t slot = sc->k & 1;
-            F.tile_cost = sc->buf + slot * sc->n;
-            if (sc->k >= 2) {  // the order launch k - 2's durations gave, once its sort has finished
-                RM_HIP(hipStreamWaitEvent(ctx->stream, sc->sorted[slot], 0));
-                F.tile_order = sc->buf + (2 + slot) * sc->n;
+            const uint64_t P = (uint64_t)sched_period(), k = sc->k;
+            if (k % P == 0) F.tile_cost = sc->buf + ((k / P) & 1) * sc->n;  // sort k / P reads them
+            if (k >= 2) {  // the newest order whose sort had a launch to overlap
+                const uint64_t s = (k - 2) / P;
+                if (k - 2 == s * P) RM_HIP(hipStreamWaitEvent(ctx->stream, sc->sorted[s & 1], 0));
+                F.tile_order = sc->buf + (2 + (s & 1)) * sc->n;
             }
         }
     }
@@ -398,8 +414,8 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
             : rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
-    if (sc) {  // sort this launch's durations on the side stream, overlapping the next launch
-        const size_t slot = sc->k & 1;
+    if (sc && F.tile_cost) {  // sort this launch's durations on the side stream, overlapping the next launch
+        const size_t slot = (sc->k / (uint64_t)sched_period()) & 1;
         uint32_t *h = sc->buf + 4 * (size_t)sc->n;
         RM_HIP(hipEventRecord(sc->rendered, ctx->stream));
         RM_HIP(hipStreamWaitEvent(ctx->side, sc->rendered, 0));
@@ -407,8 +423,8 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
                                   h + 512 * (1 - slot), ctx->side);
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
         RM_HIP(hipEventRecord(sc->sorted[slot], ctx->side));
-        sc->k++;
     }
+    if (sc) sc->k++;
     if (stats) {
         RM_HIP(hipEventSynchronize(ctx->ev1));
         float ms = 0.0f;
