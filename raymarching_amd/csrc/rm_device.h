@@ -191,23 +191,37 @@ __device__ __forceinline__ float sponge_box(V3 p) {
 // d >= 1/s the remaining folds cannot raise d (the `if (c > d)` of
 // common.frag:671 never fires) and the result is exactly d.  Lanes that are
 // not `active` never ask for a fold.  Far from the sponge (most march and
-// shadow steps) whole waves skip the folds.  (Wave-uniform variants of this
-// branch and of the march loops, __ballot-driven with lanes frozen by
-// selects, measured 1.13 ms against 0.93 ms per 4096^2 T frame: DESIGN.md.)
+// shadow steps) whole waves skip the folds.  The exit test is wave-uniform
+// (RM_FOLD_UNIFORM): a wave computes fold m if any of its lanes needs it, and
+// lanes past their exit point compute a fold that leaves d unchanged.  The
+// same VALU as a per-lane branch, without the two exec-mask SALU per test
+// (v_cmp to vcc + s_cbranch_vccz), and SALU issue is a co-bottleneck
+// (DESIGN.md 2.2).  The FLOP tally counts the folds a lane needs.
 // NB: how many of the three folds keep their exit test.  A fold computed past
 // its exit point leaves d unchanged, so any NB gives the same distance: 3 (the
 // default) executes the fewest instructions, 1 the fewest branches and exec-mask
 // updates, which is what bounds the latency of a lone long wave (the tail of a
 // launch: render_tile's latency tiles).
+#ifndef RM_FOLD_UNIFORM
+#define RM_FOLD_UNIFORM 1
+#endif
 template <bool EXACT, int NB = 3>
 __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool active = true) {
     constexpr float SH[3] = {0.5f, 1.5f, 4.5f};                      // s/2 before s *= 3
     constexpr float S3[3] = {3.0f, 9.0f, 27.0f};                     // s after s *= 3
     constexpr float INV[3] = {1.0f / 3.0f, 1.0f / 9.0f, 1.0f / 27.0f};
+    bool need = active;  // this lane's d can still change (fold m's test passed)
 #pragma unroll
     for (int m = 0; m < 3; m++) {
-        if (m < NB && !(active && d < INV[m])) return d;
-        fl += FL_FOLD;
+        if (m < NB) {
+            need = active && d < INV[m];  // (d only grows: implies the earlier tests)
+#if RM_FOLD_UNIFORM
+            if (__builtin_amdgcn_ballot_w64(need) == 0) return d;
+#else
+            if (!need) return d;
+#endif
+        }
+        if (need) fl += FL_FOLD;
         float rx, ry, rz;
         if constexpr (EXACT) {
             float hx = p.x * SH[m], hy = p.y * SH[m], hz = p.z * SH[m];

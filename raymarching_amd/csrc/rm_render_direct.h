@@ -201,9 +201,9 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // vanish: the candidate is k h / t (Q = 1, D = t below).  The occlusion result
 // is recovered after the loop from the last h (a lane leaves through
 // t >= maxt only with h >= 0.001).
-template <int NB = 3>
-__device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
-                                                Tally& cnt) {
+template <bool CAP, int NB>
+__device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const LinRay& s, float mint, float maxt,
+                                                     Tally& cnt) {
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
     float t = mint;
     // one exit test per step (occluded, t >= maxt, or the optional step cap);
@@ -219,9 +219,23 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
         den = upd ? cd : den;
         P = h + h;
         t = fmaf(h, 0.1f, t + 0.001f);
-        if ((h < 0.001f) | !(t < maxt) | (it >= F.shadow_max_steps)) break;
+        if ((h < 0.001f) | !(t < maxt) | (CAP && it >= F.shadow_max_steps)) break;
     }
     return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(16.0f * num * __builtin_amdgcn_rcpf(den));
+}
+#ifndef RM_SHADOW_UNCAPPED_LOOP
+#define RM_SHADOW_UNCAPPED_LOOP 1
+#endif
+// The uncapped loop (the reference's, and the default) carries no step
+// counter: a uniform counter test merged into the lanes' exit mask costs 5
+// SALU per step, and SALU issue is a co-bottleneck of the kernel.
+template <int NB = 3>
+__device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
+                                                Tally& cnt) {
+#if RM_SHADOW_UNCAPPED_LOOP
+    if (F.shadow_max_steps == __INT_MAX__) return soft_shadow2_T_loop<false, NB>(F, s, mint, maxt, cnt);
+#endif
+    return soft_shadow2_T_loop<true, NB>(F, s, mint, maxt, cnt);
 }
 
 // castRay (common.frag:931-954) for scene T in sponge space; returns the
