@@ -111,9 +111,10 @@ rm_status rm_scene_eval(rm_ctx *ctx, const float *points, int64_t n, float *dist
 /* Replace sf::Shader::setUniform (include/SFML/Graphics/Shader.hpp:297,306,315)
  * for the names main.cpp sets: u_resolution (2f), u_pos (3f), u_mouse (2f),
  * u_time (1f), u_sample_part (1f), u_seed1/u_seed2 (2f).  The last three are
- * declared but unused by the scenes (common.frag:8-11) and are accepted and
- * ignored; other names warn once on stderr and are ignored, as SFML does for
- * uniforms the GLSL compiler removed.  Wrong arity -> RM_ERR_INVALID_ARGUMENT. */
+ * declared but unused by the reference's scenes (common.frag:8-11): the plain
+ * renders ignore them and rm_render_accumulate* reads them.  Other names warn
+ * once on stderr and are ignored, as SFML does for uniforms the GLSL compiler
+ * removed.  Wrong arity -> RM_ERR_INVALID_ARGUMENT. */
 rm_status rm_set_uniform1f(rm_ctx *ctx, const char *name, float x);
 rm_status rm_set_uniform2f(rm_ctx *ctx, const char *name, float x, float y);
 rm_status rm_set_uniform3f(rm_ctx *ctx, const char *name, float x, float y, float z);
@@ -193,6 +194,21 @@ rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t 
  * pixel as rm_pack_rgba8 does (bit-identical to rm_render + rm_pack_rgba8),
  * writing 4 B/px instead of 16. */
 rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats);
+
+/* Progressive accumulation: the reference's ping-pong plumbing (main.cpp:192-207:
+ * u_sample = the previous output texture, u_sample_part = 1/framesStill, fresh
+ * u_seed1/u_seed2 per frame; common.frag:8-11), which its shaders declare but
+ * never read, as a pass that reads it.  `accum` (W*H float4, or RGBA8 words for
+ * the _rgba8 call; device or host) holds u_sample, the previous frame, and
+ * receives mix(u_sample, colour, u_sample_part) per pixel, where the colour is
+ * the pass's with the fragment moved by the sub-pixel offset fract(u_seed1) -
+ * 0.5 (GLSL fract): with main.cpp's uniforms, accum is the running mean of the
+ * jittered frames since the camera stopped (progressive supersampling).
+ * u_sample_part >= 1 stores the colour (accum needs no clearing); with
+ * u_seed1 = (0.5, 0.5) and u_sample_part = 1 the result is rm_render's /
+ * rm_render_rgba8's, bit for bit. */
+rm_status rm_render_accumulate(rm_ctx *ctx, int W, int H, float *accum, rm_stats *stats);
+rm_status rm_render_accumulate_rgba8(rm_ctx *ctx, int W, int H, uint32_t *accum, rm_stats *stats);
 
 /* rm_render_band / rm_render_rows into RGBA8 rows (W uint32 per row). */
 rm_status rm_render_band_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, uint32_t *out,

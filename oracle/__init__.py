@@ -34,6 +34,7 @@ class OracleUniforms(ctypes.Structure):
         ("time", ctypes.c_float),
         ("max_steps", ctypes.c_int32),
         ("shadow_max_steps", ctypes.c_int32),
+        ("jit_x", ctypes.c_float), ("jit_y", ctypes.c_float),
     ]
 
 
@@ -93,11 +94,48 @@ def lib(fast: bool = False) -> ctypes.CDLL:
 
 
 def uniforms(W, H, pos=(2.0, 3.0, 3.0), mouse=(0.0, 0.0), time=0.0, max_steps=128,
-             shadow_max_steps=0, res=None) -> OracleUniforms:
+             shadow_max_steps=0, res=None, jitter=(0.0, 0.0)) -> OracleUniforms:
     rx, ry = (W, H) if res is None else res
     return OracleUniforms(float(rx), float(ry), float(mouse[0]), float(mouse[1]), float(pos[0]),
                           float(pos[1]), float(pos[2]), float(time), int(max_steps),
-                          int(shadow_max_steps))
+                          int(shadow_max_steps), float(jitter[0]), float(jitter[1]))
+
+
+def seed_jitter(seed1):
+    """The sub-pixel offset progressive accumulation renders with (rm.h
+    rm_render_accumulate): fract(u_seed1) - 0.5 per axis, GLSL fract, in f32."""
+    s = np.asarray(seed1, np.float32)
+    return tuple(float(v) for v in (s - np.floor(s)) - np.float32(0.5))
+
+
+def accumulate(prev, colour, part):
+    """mix(u_sample, colour, u_sample_part) as the accumulating pass stores it:
+    prev + (colour - prev) * part in f32 (each operation rounded, no FMA); part >= 1
+    stores the colour.  RGB of float32 [..., 4] arrays; alpha = 1."""
+    part = np.float32(part)
+    if part >= 1.0:
+        out = colour.astype(np.float32).copy()
+    else:
+        p = prev.astype(np.float32)
+        out = (p + (colour.astype(np.float32) - p) * part).astype(np.float32)
+    out[..., 3] = 1.0
+    return out
+
+
+def unpack_rgba8(words):
+    """RGBA8 words -> float32 [..., 4] as the accumulating pass reads u_sample:
+    b * RN(1/255)."""
+    w = np.asarray(words).astype(np.uint32)
+    k = np.float32(1.0) / np.float32(255.0)
+    return np.stack([((w >> s) & 255).astype(np.float32) * k for s in (0, 8, 16, 24)], -1)
+
+
+def pack_rgba8(rgba):
+    """float32 [..., 4] -> RGBA8 words as the kernels pack them: clamp to [0, 1]
+    (NaN -> 0), x * 255 rounded to nearest even."""
+    c = np.nan_to_num(np.clip(rgba.astype(np.float32), 0.0, 1.0), nan=0.0)
+    b = np.rint(c * np.float32(255.0)).astype(np.uint32)
+    return (b[..., 0] | (b[..., 1] << 8) | (b[..., 2] << 16) | (b[..., 3] << 24)).astype(np.uint32)
 
 
 def _p(a, t):

@@ -62,6 +62,8 @@ typedef struct {
     float time;             /* u_time       */
     int32_t max_steps;      /* MAX_MARCHING_STEPS (common.frag:15) */
     int32_t shadow_max_steps; /* 0 = unbounded, as common.frag:814 */
+    float jit_x, jit_y;     /* progressive accumulation: sub-pixel offset of the fragment
+                               (fract(u_seed1) - 0.5; 0 = the pixel centre) */
 } oracle_uniforms;
 
 typedef struct {
@@ -730,7 +732,7 @@ static vec3 render_S0(const Ctx *C, vec3 ro, vec3 rd) {
  * W x H target: gl_TexCoord = ((col+.5)/W, (row+.5)/H) (row 0 first in
  * memory). */
 static void shade_pixel(const Ctx *C, int W, int H, int col, int row, float *out4) {
-    vec2 tc = {((float)col + 0.5f) / (float)W, ((float)row + 0.5f) / (float)H};
+    vec2 tc = {((float)col + 0.5f + C->u.jit_x) / (float)W, ((float)row + 0.5f + C->u.jit_y) / (float)H};
     vec2 uv = {(tc.x - 0.5f) * C->u.res_x / C->u.res_y, (tc.y - 0.5f) * C->u.res_y / C->u.res_y};
     vec3 ro = v3(C->u.pos_x, C->u.pos_y, C->u.pos_z);
     vec3 rd = normalize3(v3(uv.x, -uv.y, -1.0f));

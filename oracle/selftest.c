@@ -15,6 +15,7 @@
 typedef struct {
     float res_x, res_y, mouse_x, mouse_y, pos_x, pos_y, pos_z, time;
     int32_t max_steps, shadow_max_steps;
+    float jit_x, jit_y;
 } oracle_uniforms;
 
 int oracle_render(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, float *out, uint32_t *evals);
@@ -32,7 +33,7 @@ int main(void) {
             for (int scene = 0; scene < 4; scene++) {
                 const int W = sizes[si][0], H = sizes[si][1];
                 const float *p = poses[pi];
-                oracle_uniforms u = {(float)W, (float)H, p[3], p[4], p[0], p[1], p[2], p[5], 64, scene == 2 ? 32 : 0};
+                oracle_uniforms u = {(float)W, (float)H, p[3], p[4], p[0], p[1], p[2], p[5], 64, scene == 2 ? 32 : 0, 0.0f, 0.0f};
                 float *img = malloc(sizeof(float) * 4 * W * H);
                 uint32_t *ev = malloc(sizeof(uint32_t) * W * H);
                 if (oracle_render(scene, &u, W, H, 0, H, img, ev)) return 1;

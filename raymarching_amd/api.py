@@ -135,6 +135,21 @@ class Renderer:
               self._ctx)
         return (out, s.as_dict()) if stats else out
 
+    def render_accumulate(self, W: int, H: int, accum, stats: bool = False):
+        """Progressive accumulation (rm_render_accumulate[_rgba8]): `accum` holds
+        the previous frame (u_sample) and receives mix(u_sample, colour,
+        u_sample_part), the colour rendered with the sub-pixel offset
+        fract(u_seed1) - 0.5.  float32 [H, W, 4] or RGBA8 int32 [H, W] words."""
+        torch = _torch()
+        rgba8 = accum.dtype == torch.int32
+        if not rgba8 and accum.dtype != torch.float32:
+            raise ValueError("render_accumulate: accum must be float32 [H, W, 4] or int32 RGBA8 words [H, W]")
+        _check_out(accum, H * W * (1 if rgba8 else 4))
+        s = RmStats()
+        fn = lib().rm_render_accumulate_rgba8 if rgba8 else lib().rm_render_accumulate
+        check(fn(self._ctx, int(W), int(H), self._ptr(accum), ctypes.byref(s) if stats else None), self._ctx)
+        return (accum, s.as_dict()) if stats else accum
+
     def render_step_map(self, W: int, H: int, out=None, evals_map=None):
         """Full frame plus the per-pixel sceneSDF call counts: (float32 [H, W, 4],
         int32 [H, W], stats), device tensors (allocated if None)."""

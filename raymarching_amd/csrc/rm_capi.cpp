@@ -39,6 +39,8 @@ struct rm_ctx {
     float pos[3] = {0.0f, 0.0f, 0.0f};
     float mouse[2] = {0.0f, 0.0f};
     float time = 0.0f;
+    float sample_part = 1.0f;  // u_sample_part, u_seed1, u_seed2: read by rm_render_accumulate*
+    float seed1[2] = {0.0f, 0.0f}, seed2[2] = {0.0f, 0.0f};
     rm_params params = {128, 0, 0, 0, 1};
     std::string err;
     std::set<std::string> warned;
@@ -381,11 +383,17 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
 }
 
 rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, void *out,
-                     bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr) {
+                     bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
     rm::TraceRange range("rm_render");
     FrameConst F = frame_const(ctx, W, H, band, nshards, shard, count);
     F.row0 = row0;
     F.evals_map = evmap;
+    if (accum) {  // fract(u_seed1) - 0.5 (GLSL fract, x - floor(x)), per frame
+        F.accumulate = 1;
+        F.sample_part = ctx->sample_part;
+        F.jit_x = (ctx->seed1[0] - std::floor(ctx->seed1[0])) - 0.5f;
+        F.jit_y = (ctx->seed1[1] - std::floor(ctx->seed1[1])) - 0.5f;
+    }
     rm_ctx::Sched *sc = nullptr;
     if (ctx->tile_order) {  // an explicit order wins
         const rm::TileGrid g =
@@ -442,7 +450,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
 
 // row_count < 0: every packed row from row_begin on; out: float4 or RGBA8 rows
 rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
-                     void *out, bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr) {
+                     void *out, bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
@@ -462,7 +470,7 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     RM_HIP(hipSetDevice(ctx->device));
     const bool dev_out = is_device_ptr(out), dev_map = !evmap || is_device_ptr(evmap);
     if (dev_out && dev_map)
-        return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, out, rgba8, stats, evmap);
+        return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, out, rgba8, stats, evmap, accum);
     // host buffers go through the staging buffer: the frame, then the step map
     const size_t bytes = dev_out ? 0 : (size_t)W * row_count * (rgba8 ? sizeof(uint32_t) : sizeof(float4));
     const size_t map_bytes = dev_map ? 0 : (size_t)W * row_count * sizeof(uint32_t);
@@ -470,7 +478,9 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     if (s != RM_OK) return s;
     char *st = reinterpret_cast<char *>(ctx->staging);
     uint32_t *map_d = dev_map ? evmap : reinterpret_cast<uint32_t *>(st + bytes);
-    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, dev_out ? out : st, rgba8, stats, map_d);
+    if (accum && !dev_out) RM_HIP(hipMemcpyAsync(st, out, bytes, hipMemcpyHostToDevice, ctx->stream));  // u_sample
+    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, dev_out ? out : st, rgba8, stats, map_d,
+                   accum);
     if (s != RM_OK) return s;
     if (!dev_out) RM_HIP(hipMemcpyAsync(out, st, bytes, hipMemcpyDeviceToHost, ctx->stream));
     if (!dev_map) RM_HIP(hipMemcpyAsync(evmap, map_d, map_bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -629,7 +639,11 @@ static rm_status set_uniform(rm_ctx *ctx, const char *name, int n, float x, floa
         else if (nm == "u_pos") { ctx->pos[0] = x; ctx->pos[1] = y; ctx->pos[2] = z; }
         else if (nm == "u_mouse") { ctx->mouse[0] = x; ctx->mouse[1] = y; }
         else if (nm == "u_time") ctx->time = x;
-        // u_sample_part, u_seed1, u_seed2: declared, unused by the pass (common.frag:8-11)
+        // u_sample_part, u_seed1, u_seed2: declared, unused by the reference's pass
+        // (common.frag:8-11); rm_render_accumulate* reads them
+        else if (nm == "u_sample_part") ctx->sample_part = x;
+        else if (nm == "u_seed1") { ctx->seed1[0] = x; ctx->seed1[1] = y; }
+        else if (nm == "u_seed2") { ctx->seed2[0] = x; ctx->seed2[1] = y; }
         return RM_OK;
     }
     if (ctx->warned.insert(nm).second) std::fprintf(stderr, "rm: uniform \"%s\" not found in shader\n", name);
@@ -692,6 +706,14 @@ rm_status rm_render_rows(rm_ctx *ctx, int W, int H, int band, int nshards, int s
 
 rm_status rm_render_rgba8(rm_ctx *ctx, int W, int H, uint32_t *out, rm_stats *stats) {
     return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, out, true, stats);
+}
+
+rm_status rm_render_accumulate(rm_ctx *ctx, int W, int H, float *accum, rm_stats *stats) {
+    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, accum, false, stats, nullptr, true);
+}
+
+rm_status rm_render_accumulate_rgba8(rm_ctx *ctx, int W, int H, uint32_t *accum, rm_stats *stats) {
+    return render_any(ctx, W, H, H > 0 ? H : 1, 1, 0, 0, -1, accum, true, stats, nullptr, true);
 }
 
 rm_status rm_render_band_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, uint32_t *out,

@@ -58,6 +58,10 @@ struct FrameConst {
     uint32_t* tile_cost;           // if set: each one-wave tile's duration in shader clocks (adaptive order)
     int lat_tiles;                 // with tile_order: the first lat_tiles workgroups (the costliest tiles) render
                                    // with the latency-optimized Menger folds (scene T, render_tile)
+    int accumulate;                // rm_render_accumulate*: out holds u_sample (this pixel of the previous frame)
+                                   // and receives mix(u_sample, colour, sample_part)
+    float sample_part;             // u_sample_part
+    float jit_x, jit_y;            // with accumulate: sub-pixel offset of the fragment, fract(u_seed1) - 0.5
 };
 
 // Buckets of the adaptive dispatch order (rm_capi.cpp, rm_kernels.hip): 256

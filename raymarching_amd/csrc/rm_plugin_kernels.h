@@ -46,8 +46,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R
         const float vig = vignette<false>(tcx, tcy);
         V3 c = post_colour<false>(render_pixel<SCENE_PLUGIN>(F, ro, rd, cnt), vig);
         const size_t i = (size_t)j * F.W + x;
-        if (rgba8) static_cast<uint32_t*>(out)[i] = pack_rgba8(c.x, c.y, c.z, 1.0f);
-        else static_cast<float4*>(out)[i] = make_float4(c.x, c.y, c.z, 1.0f);
+        if (rgba8) store_pixel(F, static_cast<uint32_t*>(out), i, c);
+        else store_pixel(F, static_cast<float4*>(out), i, c);
     }
     if (F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
         const uint64_t dt = clock64() - t_start;

@@ -494,8 +494,8 @@ __device__ __forceinline__ V3 render_S0(const FrameConst& F, V3 ro, V3 rd, Tally
 
 // Camera (output_shader.frag:388-404): gl_TexCoord at the pixel centre
 __device__ __forceinline__ void camera_ray(const FrameConst& F, int x, int y, float& tcx, float& tcy, V3& ro, V3& rd) {
-    tcx = ((float)x + 0.5f) / (float)F.W;
-    tcy = ((float)y + 0.5f) / (float)F.H;
+    tcx = ((float)x + 0.5f + F.jit_x) / (float)F.W;  // (jitter 0 outside rm_render_accumulate*)
+    tcy = ((float)y + 0.5f + F.jit_y) / (float)F.H;
     float ux = (tcx - 0.5f) * F.res_x / F.res_y;
     float uy = (tcy - 0.5f) * F.res_y / F.res_y;
     ro = v3(F.pos_x, F.pos_y, F.pos_z);
@@ -506,6 +506,35 @@ __device__ __forceinline__ void camera_ray(const FrameConst& F, int x, int y, fl
     float x2 = rd.x * F.cam2_c + z1 * -F.cam2_s;
     float z2 = rd.x * F.cam2_s + z1 * F.cam2_c;
     rd = v3(x2, y1, z2);
+}
+
+// The pixel store of a render launch.  With F.accumulate (progressive
+// accumulation, rm_render_accumulate*: the ping-pong u_sample plumbing of
+// main.cpp:192-207 and common.frag:8-11, read by the pass) the target holds
+// u_sample, this pixel of the previous frame, and receives
+// mix(u_sample, colour, u_sample_part) (GLSL mix as the fixture renderer
+// evaluates it, x + (y - x) a, no contraction); RGBA8 targets are read as GL
+// reads unorm8 texels, b * RN(1/255) (within 1 ulp of b / 255).  A part >= 1
+// (the first frame of a still camera) stores the colour: the target needs no
+// clearing.
+template <typename OUT>
+__device__ __forceinline__ void store_pixel(const FrameConst& F, OUT* __restrict__ out, size_t i, V3 c) {
+#pragma clang fp contract(off)
+    if (F.accumulate && F.sample_part < 1.0f) {
+        V3 prev;
+        if constexpr (sizeof(OUT) == 4) {
+            const uint32_t w = out[i];
+            const float k = 1.0f / 255.0f;
+            prev = v3((float)(w & 255u) * k, (float)((w >> 8) & 255u) * k, (float)((w >> 16) & 255u) * k);
+        } else {
+            const float4 v = out[i];
+            prev = v3(v.x, v.y, v.z);
+        }
+        const float a = F.sample_part;
+        c = v3(prev.x + (c.x - prev.x) * a, prev.y + (c.y - prev.y) * a, prev.z + (c.z - prev.z) * a);
+    }
+    if constexpr (sizeof(OUT) == 4) out[i] = pack_rgba8(c.x, c.y, c.z, 1.0f);
+    else out[i] = make_float4(c.x, c.y, c.z, 1.0f);
 }
 
 // local packed row j of this shard -> frame row y
@@ -597,8 +626,7 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
             c = render_pixel<SC>(F, ro, rd, cnt);
         }
         c = post_colour<FastMath<SC>::value>(c, vig);
-        if constexpr (sizeof(OUT) == 4) out[(size_t)j * F.W + x] = pack_rgba8(c.x, c.y, c.z, 1.0f);
-        else out[(size_t)j * F.W + x] = make_float4(c.x, c.y, c.z, 1.0f);
+        store_pixel(F, out, (size_t)j * F.W + x, c);
     }
     if (T::WPB == 1 && F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
         const uint64_t dt = clock64() - t_start;

@@ -1,0 +1,149 @@
+"""Progressive accumulation (rm_render_accumulate[_rgba8]): the reference's
+ping-pong u_sample / u_sample_part / u_seed plumbing (main.cpp:192-207,
+common.frag:8-11) as a pass that reads it.  The reference's shaders never read
+u_sample, so there is no reference output to pin beyond its identities: the
+first frame of a still camera (u_sample_part = 1) with a zero sub-pixel offset
+is the plain pass bit for bit (pinned by the goldens through rm_render), and a
+jittered, accumulated sequence equals the oracle's jittered frames blended with
+the same f32 arithmetic (oracle.accumulate)."""
+import numpy as np
+import pytest
+
+import oracle
+import raymarching_amd as rm
+from raymarching_amd import POSES
+from tests.parity import assert_parity
+
+
+def test_accumulate_host_arithmetic():
+    """oracle.accumulate / pack / unpack: the pass's f32 semantics (CPU)."""
+    rng = np.random.default_rng(1)
+    prev = rng.random((5, 7, 4), np.float32)
+    col = rng.random((5, 7, 4), np.float32)
+    # part >= 1 stores the colour; mix of equal frames is the frame (x + 0 * a)
+    assert np.array_equal(oracle.accumulate(prev, col, 1.0)[..., :3], col[..., :3])
+    assert np.array_equal(oracle.accumulate(col, col, 0.25)[..., :3], col[..., :3])
+    a = oracle.accumulate(prev, col, np.float32(1.0) / np.float32(3.0))
+    exp = prev[..., :3] + (col[..., :3] - prev[..., :3]) * (np.float32(1.0) / np.float32(3.0))
+    assert np.array_equal(a[..., :3], exp) and a.dtype == np.float32
+    # every byte survives unpack -> pack
+    w = np.arange(256, dtype=np.uint32) * 0x01010101
+    assert np.array_equal(oracle.pack_rgba8(oracle.unpack_rgba8(w)), w)
+    assert oracle.seed_jitter((0.5, 1.5)) == (0.0, 0.0)
+    assert oracle.seed_jitter((0.25, 998.75)) == (-0.25, 0.25)
+
+
+def test_oracle_jitter_zero_is_the_pixel_centre():
+    """A zero offset leaves the oracle's fragment coordinates (and so every
+    golden) unchanged; a non-zero one moves the image (CPU)."""
+    p = POSES["P0"]
+    kw = dict(pos=p["pos"], mouse=p["mouse"], time=p["time"], max_steps=64)
+    a, ea = oracle.render("T", 24, 16, **kw)
+    b, eb = oracle.render("T", 24, 16, jitter=(0.0, 0.0), **kw)
+    c, _ = oracle.render("T", 24, 16, jitter=(0.25, -0.25), **kw)
+    assert np.array_equal(a, b) and np.array_equal(ea, eb)
+    assert not np.array_equal(a, c)
+
+
+# ------------------------------------------------------------------ GPU
+
+
+@pytest.fixture(scope="module")
+def R(torch_cuda):
+    r = rm.Renderer(0)
+    yield r
+    r.close()
+
+
+def _setup(r, scene, pose, steps):
+    r.load_scene(rm.SCENE_FILES[scene])
+    r.set_pose(pose["pos"], pose["mouse"], pose["time"])
+    r.set_params(max_steps=steps, shadow_max_steps=0, count_evals=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["T", "O"])
+def test_first_frame_is_the_plain_pass(R, torch_cuda, scene):
+    """u_sample_part = 1 and u_seed1 = (0.5, 0.5): rm_render's / rm_render_rgba8's
+    frame bit for bit, whatever the target held (it is not read)."""
+    torch = torch_cuda
+    _setup(R, scene, POSES["P2"], 128)
+    W, H = 61, 37
+    plain = R.render(W, H)
+    plain8 = R.render_rgba8(W, H)
+    R.set_uniform("u_seed1", 0.5, 0.5)
+    R.set_uniform("u_sample_part", 1.0)
+    acc = torch.full((H, W, 4), float("nan"), device="cuda")
+    R.render_accumulate(W, H, acc)
+    assert torch.equal(acc, plain)
+    acc8 = torch.full((H, W), -1, dtype=torch.int32, device="cuda")
+    R.render_accumulate(W, H, acc8)
+    assert torch.equal(acc8, plain8)
+
+
+SEEDS = [(0.5, 0.5), (17.25, 3.75), (998.875, 40.125), (0.625, 512.375)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,W,H,steps", [("T", 64, 48, 128), ("O", 48, 32, 128)])
+def test_accumulated_sequence_vs_oracle(R, torch_cuda, scene, W, H, steps):
+    """Four still-camera frames as main.cpp drives them (u_sample_part =
+    1/framesStill, a fresh u_seed1 per frame) against the oracle's jittered
+    frames blended in f32: the scene's parity policy on every intermediate
+    accumulator."""
+    torch = torch_cuda
+    pose = POSES["P3"]
+    _setup(R, scene, pose, steps)
+    acc = torch.zeros((H, W, 4), device="cuda")
+    ref = None
+    for k, seed in enumerate(SEEDS, start=1):
+        part = np.float32(1.0) / np.float32(k)
+        R.set_uniform("u_seed1", *seed)
+        R.set_uniform("u_sample_part", float(part))
+        R.render_accumulate(W, H, acc)
+        torch.cuda.synchronize()
+        frame, _ = oracle.render(scene, W, H, pos=pose["pos"], mouse=pose["mouse"], time=pose["time"],
+                                 max_steps=steps, jitter=oracle.seed_jitter(seed))
+        ref = oracle.accumulate(ref, frame, part) if ref is not None else oracle.accumulate(frame, frame, 1.0)
+        assert_parity(scene, acc.cpu().numpy(), ref, label=f"frame {k}")
+    # supersampling: the accumulator differs from any single frame on edges
+    R.set_uniform("u_seed1", 0.5, 0.5)
+    single = R.render(W, H)
+    assert not torch.equal(acc, single)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["T", "O"])
+def test_rgba8_accumulation_bit_exact(R, torch_cuda, scene):
+    """The RGBA8 target reads u_sample as unorm8 and repacks: bit-exact against
+    the host restatement fed with the GPU's own jittered colour."""
+    torch = torch_cuda
+    _setup(R, scene, POSES["P1"], 96)
+    W, H = 40, 24
+    acc8 = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+    for k, seed in enumerate(SEEDS, start=1):
+        part = np.float32(1.0) / np.float32(k)
+        R.set_uniform("u_seed1", *seed)
+        R.set_uniform("u_sample_part", 1.0)
+        colour = R.render_accumulate(W, H, torch.empty((H, W, 4), device="cuda")).cpu().numpy()
+        prev = acc8.cpu().numpy().view(np.uint32)
+        R.set_uniform("u_sample_part", float(part))
+        R.render_accumulate(W, H, acc8)
+        exp = oracle.pack_rgba8(oracle.accumulate(oracle.unpack_rgba8(prev), colour, part))
+        assert np.array_equal(acc8.cpu().numpy().view(np.uint32), exp), k
+
+
+@pytest.mark.gpu
+def test_host_accumulator_equals_device(R, torch_cuda):
+    """A host accumulator goes through the staging buffer: same bits."""
+    torch = torch_cuda
+    _setup(R, "T", POSES["P0"], 64)
+    W, H = 33, 20
+    dev = torch.zeros((H, W, 4), device="cuda")
+    host = np.zeros((H, W, 4), np.float32)
+    for k, seed in enumerate(SEEDS[:3], start=1):
+        R.set_uniform("u_seed1", *seed)
+        R.set_uniform("u_sample_part", 1.0 / k)
+        R.render_accumulate(W, H, dev)
+        rm.lib().rm_render_accumulate(R._ctx, W, H, host.ctypes.data, None)
+    assert np.array_equal(dev.cpu().numpy(), host)
