@@ -11,7 +11,7 @@
 //
 // Usage: raymarch_headless [--scene output_shader.frag] [--w 1600] [--h 900]
 //          [--frames 60] [--script WWWWDD..] [--mouse 3,0] [--time-freeze]
-//          [--steps 128] [--ppm out.ppm] [--gpus N] [--band 16]
+//          [--steps 128] [--ppm out.ppm] [--gpus N] [--band 16] [--accumulate]
 // --gpus N renders each frame's row bands on GPUs 0..N-1 and gathers them over
 // RCCL to GPU 0 (rm::ShardedRenderTexture -> rm_render_sharded_all); --sharded
 // takes that path with one GPU too.
@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
     std::string scene = "output_shader.frag", script, ppm;
     int w = 1600, h = 900, frames = 60, steps = 128, gpus = 1, band = 16;
     int mdx = 0, mdy = 0;
-    bool time_freeze = false, sharded = false;
+    bool time_freeze = false, sharded = false, accumulate = false;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() { return i + 1 < argc ? std::string(argv[++i]) : std::string(); };
@@ -46,6 +46,7 @@ int main(int argc, char** argv) {
         else if (a == "--ppm") ppm = next();
         else if (a == "--time-freeze") time_freeze = true;
         else if (a == "--sharded") sharded = true;
+        else if (a == "--accumulate") accumulate = true;
         else if (a == "--mouse") std::sscanf(next().c_str(), "%d,%d", &mdx, &mdy);
         else {
             std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -61,6 +62,10 @@ int main(int argc, char** argv) {
 
     if (gpus < 1) {
         std::fprintf(stderr, "--gpus must be >= 1\n");
+        return 2;
+    }
+    if (accumulate && (gpus > 1 || sharded)) {
+        std::fprintf(stderr, "--accumulate renders on one GPU\n");
         return 2;
     }
     // one shader (librm context) per GPU; the first is the reference's `shader`
@@ -126,7 +131,12 @@ int main(int argc, char** argv) {
         setAll("u_seed1", seed1);
         setAll("u_seed2", seed2);
         std::vector<rm_stats> st(gpus);
-        if (!sharded ? !outputTexture.draw(shader, st.data()) : !shardedTexture.draw(st.data())) {
+        // --accumulate: the pass reads u_sample/u_sample_part/u_seed1 (progressive
+        // supersampling while the camera is still; one GPU)
+        const bool drawn = sharded      ? shardedTexture.draw(st.data())
+                           : accumulate ? outputTexture.drawAccumulate(shader, st.data())
+                                        : outputTexture.draw(shader, st.data());
+        if (!drawn) {
             std::fprintf(stderr, "draw failed: %s\n", shader.lastError().c_str());
             return 1;
         }

@@ -93,6 +93,12 @@ public:
     bool draw(Shader& shader, rm_stats* stats = nullptr) {
         return tex_ && rm_render(shader.ctx(), w_, h_, tex_, stats) == RM_OK;
     }
+    // The same draw reading the ping-pong plumbing (u_sample = this texture,
+    // u_sample_part, u_seed1; main.cpp:192-207): progressive accumulation
+    // (rm_render_accumulate).  In place: each pixel reads only itself.
+    bool drawAccumulate(Shader& shader, rm_stats* stats = nullptr) {
+        return tex_ && rm_render_accumulate(shader.ctx(), w_, h_, tex_, stats) == RM_OK;
+    }
     float* texture() { return tex_; }
     int width() const { return w_; }
     int height() const { return h_; }

@@ -147,3 +147,29 @@ def test_host_accumulator_equals_device(R, torch_cuda):
         R.render_accumulate(W, H, dev)
         rm.lib().rm_render_accumulate(R._ctx, W, H, host.ctypes.data, None)
     assert np.array_equal(dev.cpu().numpy(), host)
+
+
+@pytest.mark.gpu
+def test_headless_host_accumulates(tmp_path, torch_cuda):
+    """apps/raymarch_headless --accumulate: main.cpp's loop driving the
+    plumbing (u_sample_part = 1/framesStill, fresh u_seed1 per frame) through
+    rm::RenderTexture::drawAccumulate.  Six still frames average six sub-pixel
+    offsets: away from edges the mean is the pixel-centre frame of the oracle,
+    on edges it is antialiased (differs)."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(__file__)), "apps", "raymarch_headless")
+    ppm = tmp_path / "acc.ppm"
+    out = subprocess.run([exe, "--scene", "template.frag", "--w", "96", "--h", "54", "--frames", "6", "--script",
+                          "W", "--time-freeze", "--accumulate", "--ppm", str(ppm)], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    data = ppm.read_bytes()
+    img = np.frombuffer(data[data.index(b"255\n") + 4:], np.uint8).reshape(54, 96, 3).astype(np.float32) / 255.0
+    pos = [np.float32(v) for v in info["pos"]]
+    o, _ = oracle.render("T", 96, 54, pos=pos, mouse=(0.0, 0.0), time=0.0, max_steps=128, res=(96.0, 54.0))
+    d = np.abs(img - np.clip(o[..., :3], 0, 1)).max(-1)
+    assert np.mean(d <= 3.0 / 255.0) >= 0.5, float(np.mean(d <= 3.0 / 255.0))
+    assert 1e-3 < float(d.mean()) < 0.05, float(d.mean())
