@@ -50,7 +50,8 @@ typedef struct rm_params {
     int32_t max_steps;        /* MAX_MARCHING_STEPS, common.frag:15 (default 128)        */
     int32_t shadow_max_steps; /* softshadow2 cap; 0 = unbounded as common.frag:814       */
     int32_t count_evals;      /* 1: instrumented kernel, rm_stats.evals = sceneSDF calls */
-    int32_t kernel;           /* workgroup tiling: 0 auto (= 2), 1 16x16 px (4 waves), 2 8x8 px (1 wave), 3 16x4 px (1 wave) */
+    int32_t kernel;           /* workgroup tiling: 0 auto (= 2), 1 16x16 px (4 waves), 2 8x8 px (1 wave), 3 16x4 px (1 wave),
+                                 4 8x8 px tiles pulled by persistent waves from an atomic counter (built-in scenes) */
     int32_t schedule;         /* dispatch order of one-wave tiles: 1 (default) = the costliest tiles of a recent
                                  launch of the same geometry on the same stream first (their measured durations,
                                  counting-sorted on the GPU after every 4th launch, RM_SCHED_PERIOD); 0 = row-major.

@@ -87,7 +87,7 @@ class Renderer:
         if count_evals is not None:
             p.count_evals = int(bool(count_evals))
         if kernel is not None:
-            p.kernel = {"auto": 0, "tile16": 1, "tile8": 2, "tile16x4": 3}.get(kernel, kernel)
+            p.kernel = {"auto": 0, "tile16": 1, "tile8": 2, "tile16x4": 3, "persist": 4}.get(kernel, kernel)
         check(lib().rm_set_params(self._ctx, ctypes.byref(p)), self._ctx)
 
     def params(self) -> RmParams:

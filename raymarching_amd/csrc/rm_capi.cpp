@@ -39,6 +39,8 @@ struct rm_ctx {
     float pos[3] = {0.0f, 0.0f, 0.0f};
     float mouse[2] = {0.0f, 0.0f};
     float time = 0.0f;
+    uint32_t *persist = nullptr;  // KERNEL_PERSIST: kPersistSlots pairs of self-resetting tile counters
+    uint64_t persist_k = 0;       // launches that used them (slot = persist_k % kPersistSlots)
     float sample_part = 1.0f;  // u_sample_part, u_seed1, u_seed2: read by rm_render_accumulate*
     float seed1[2] = {0.0f, 0.0f}, seed2[2] = {0.0f, 0.0f};
     rm_params params = {128, 0, 0, 0, 1};
@@ -262,6 +264,8 @@ int lat_tiles() {
 // the duration stores, the sort and the cross-stream events run on one launch
 // in four (C3 frame 0.683 -> 0.672 ms).  RM_SCHED_PERIOD
 // overrides it (1 = re-sort after every launch).
+constexpr int kPersistSlots = 8;
+
 int sched_period() {
     static const int n = [] {
         const char *e = std::getenv("RM_SCHED_PERIOD");
@@ -325,6 +329,7 @@ rm_status ensure_staging(rm_ctx *ctx, size_t bytes) {
 int pick_kernel(const rm_ctx *c) {
     if (c->params.kernel == 1) return rm::KERNEL_TILE16;
     if (c->params.kernel == 3) return rm::KERNEL_TILE16X4;
+    if (c->params.kernel == 4) return rm::KERNEL_PERSIST;
     return rm::KERNEL_TILE8;  // 0 auto, 2: measured fastest on every config
 }
 
@@ -348,7 +353,9 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
                           rm_status &st) {
     st = RM_OK;
     // plugins always launch one-wave 8x8 tiles (rm_plugin_kernels.h)
-    if (!ctx->params.schedule || (ctx->scene != rm::SCENE_PLUGIN && pick_kernel(ctx) != rm::KERNEL_TILE8)) return nullptr;
+    if (!ctx->params.schedule ||
+        (ctx->scene != rm::SCENE_PLUGIN && pick_kernel(ctx) != rm::KERNEL_TILE8 && pick_kernel(ctx) != rm::KERNEL_PERSIST))
+        return nullptr;
     const rm::TileGrid g = rm::tile_grid(rm::KERNEL_TILE8, W, count);
     const int n = g.x * g.y;
     uint64_t key = 0xcbf29ce484222325ULL;
@@ -412,6 +419,18 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
                 F.tile_order = sc->buf + (2 + (s & 1)) * sc->n;
             }
         }
+    }
+    if (ctx->scene != rm::SCENE_PLUGIN && pick_kernel(ctx) == rm::KERNEL_PERSIST) {
+        // counters zeroed once; each launch leaves its pair zeroed.  Launches
+        // of one ctx on different streams use different pairs while fewer than
+        // kPersistSlots are in flight.
+        if (!ctx->persist) {
+            const size_t bytes = (size_t)rm::kPersistWords * kPersistSlots * sizeof(uint32_t);
+            RM_HIP(hipMalloc(&ctx->persist, bytes));
+            RM_HIP(hipMemsetAsync(ctx->persist, 0, bytes, ctx->stream));
+            RM_HIP(hipStreamSynchronize(ctx->stream));  // zero before any stream's first launch
+        }
+        F.persist = ctx->persist + (size_t)rm::kPersistWords * (ctx->persist_k++ % kPersistSlots);
     }
     bool cnt = ctx->params.count_evals != 0 || evmap;
     if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 2 * sizeof(unsigned long long), ctx->stream));
@@ -570,6 +589,7 @@ rm_status rm_destroy(rm_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);  // nothing of this context still runs
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
+    if (ctx->persist) (void)hipFree(ctx->persist);
     if (ctx->staging) (void)hipFree(ctx->staging);
     if (ctx->mips) (void)hipFree(ctx->mips);
     if (ctx->tile_order) (void)hipFree(ctx->tile_order);
@@ -660,7 +680,7 @@ rm_status rm_set_uniform3f(rm_ctx *ctx, const char *name, float x, float y, floa
 
 rm_status rm_set_params(rm_ctx *ctx, const rm_params *p) {
     if (!ctx || !p) return RM_ERR_INVALID_ARGUMENT;
-    if (p->max_steps < 0 || p->max_steps > (1 << 20) || p->shadow_max_steps < 0 || p->kernel < 0 || p->kernel > 3 ||
+    if (p->max_steps < 0 || p->max_steps > (1 << 20) || p->shadow_max_steps < 0 || p->kernel < 0 || p->kernel > 4 ||
         p->schedule < 0 || p->schedule > 1)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_set_params: out of range");
     ctx->params = *p;

@@ -62,6 +62,7 @@ struct FrameConst {
                                    // and receives mix(u_sample, colour, sample_part)
     float sample_part;             // u_sample_part
     float jit_x, jit_y;            // with accumulate: sub-pixel offset of the fragment, fract(u_seed1) - 0.5
+    uint32_t* persist;             // KERNEL_PERSIST: {next dispatch ordinal, waves done}, zero between launches
 };
 
 // Buckets of the adaptive dispatch order (rm_capi.cpp, rm_kernels.hip): 256

@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rm_device.h"
 #include "rm_launch.h"
 #include "rm_render_direct.h"
@@ -24,6 +26,13 @@ template <int SC, bool COUNT, int K, typename OUT>
 __global__ __launch_bounds__(64 * Tiling<K>::WPB) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<SC>)))
 void rm_render_direct(FrameConst F, OUT* __restrict__ out, unsigned long long* __restrict__ evals) {
     render_tile<SC, COUNT, K, OUT>(F, out, evals);
+}
+
+template <int SC, bool COUNT, typename OUT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<SC>)))
+void rm_render_persist(FrameConst F, OUT* __restrict__ out, unsigned long long* __restrict__ evals, int gx,
+                       int ntiles) {
+    render_persistent<SC, COUNT, OUT>(F, out, evals, gx, ntiles);
 }
 
 template <int SC>
@@ -48,8 +57,29 @@ hipError_t launch_direct(const FrameConst& F, OUT* out, unsigned long long* eval
     return hipGetLastError();
 }
 
+// As many persistent waves as the device holds at once (the occupancy of the
+// kernel on every CU), at most one per tile.
+template <int SC, typename OUT>
+hipError_t launch_persist(const FrameConst& F, OUT* out, unsigned long long* evals, hipStream_t s) {
+    if (!F.persist) return hipErrorInvalidValue;
+    const TileGrid g = tile_grid(KERNEL_PERSIST, F.W, F.nrows);
+    const int ntiles = g.x * g.y;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = evals ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rm_render_persist<SC, true, OUT>, 64, 0)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rm_render_persist<SC, false, OUT>, 64, 0);
+    if (e != hipSuccess) return e;
+    const int waves = std::max(1, std::min(ntiles, cus * std::max(per_cu, 1)));
+    if (evals) hipLaunchKernelGGL((rm_render_persist<SC, true, OUT>), dim3(waves), dim3(64), 0, s, F, out, evals, g.x, ntiles);
+    else hipLaunchKernelGGL((rm_render_persist<SC, false, OUT>), dim3(waves), dim3(64), 0, s, F, out, evals, g.x, ntiles);
+    return hipGetLastError();
+}
+
 template <int SC, typename OUT>
 hipError_t launch_tiling(const FrameConst& F, OUT* out, unsigned long long* evals, int kernel, hipStream_t s) {
+    if (kernel == KERNEL_PERSIST) return launch_persist<SC>(F, out, evals, s);
     if (kernel == KERNEL_TILE16) return launch_direct<SC, KERNEL_TILE16>(F, out, evals, s);
     if (kernel == KERNEL_TILE16X4) return launch_direct<SC, KERNEL_TILE16X4>(F, out, evals, s);
     return launch_direct<SC, KERNEL_TILE8>(F, out, evals, s);

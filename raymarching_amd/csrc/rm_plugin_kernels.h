@@ -42,7 +42,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R
         const int y = shard_row(F, F.row0 + j);
         float tcx, tcy;
         V3 ro, rd;
-        camera_ray(F, x, y, tcx, tcy, ro, rd);
+        camera_ray<false>(F, x, y, tcx, tcy, ro, rd);
         const float vig = vignette<false>(tcx, tcy);
         V3 c = post_colour<false>(render_pixel<SCENE_PLUGIN>(F, ro, rd, cnt), vig);
         const size_t i = (size_t)j * F.W + x;

@@ -492,12 +492,22 @@ __device__ __forceinline__ V3 render_S0(const FrameConst& F, V3 ro, V3 rd, Tally
     return background(ro, rd);
 }
 
-// Camera (output_shader.frag:388-404): gl_TexCoord at the pixel centre
+// Camera (output_shader.frag:388-404): gl_TexCoord at the pixel centre.
+// FAST (scenes S0/T): the divisions by the per-frame W, H and u_resolution.y
+// as v_rcp + mul, spelled out: left to -freciprocal-math, the compiler hoisted
+// a correctly rounded 1/W out of the persistent kernel's tile loop but not out
+// of the one-tile kernels, and their frames differed in a pixel.
+template <bool FAST>
 __device__ __forceinline__ void camera_ray(const FrameConst& F, int x, int y, float& tcx, float& tcy, V3& ro, V3& rd) {
-    tcx = ((float)x + 0.5f + F.jit_x) / (float)F.W;  // (jitter 0 outside rm_render_accumulate*)
-    tcy = ((float)y + 0.5f + F.jit_y) / (float)F.H;
-    float ux = (tcx - 0.5f) * F.res_x / F.res_y;
-    float uy = (tcy - 0.5f) * F.res_y / F.res_y;
+    if constexpr (FAST) {
+        tcx = ((float)x + 0.5f + F.jit_x) * __builtin_amdgcn_rcpf((float)F.W);
+        tcy = ((float)y + 0.5f + F.jit_y) * __builtin_amdgcn_rcpf((float)F.H);
+    } else {
+        tcx = ((float)x + 0.5f + F.jit_x) / (float)F.W;  // (jitter 0 outside rm_render_accumulate*)
+        tcy = ((float)y + 0.5f + F.jit_y) / (float)F.H;
+    }
+    const float ux = FAST ? (tcx - 0.5f) * F.res_x * __builtin_amdgcn_rcpf(F.res_y) : (tcx - 0.5f) * F.res_x / F.res_y;
+    const float uy = FAST ? (tcy - 0.5f) * F.res_y * __builtin_amdgcn_rcpf(F.res_y) : (tcy - 0.5f) * F.res_y / F.res_y;
     ro = v3(F.pos_x, F.pos_y, F.pos_z);
     rd = normalize(v3(ux, -uy, -1.0f));
     // rd.yz *= rot(-u_mouse.y); rd.xz *= rot(u_mouse.x)  (row vector x mat2(c,-s,s,c))
@@ -580,33 +590,37 @@ __device__ __forceinline__ void scene_eval_one(const FrameConst& F, const float*
 // of 8x8; KERNEL_TILE8 = one 8x8-pixel wave per workgroup (the dispatcher
 // then refills CUs at wave granularity, which shortens the tail of small or
 // uneven launches); KERNEL_TILE16X4 = one 16x4-pixel wave.
-enum KernelKind : int { KERNEL_TILE16 = 0, KERNEL_TILE8 = 1, KERNEL_TILE16X4 = 2 };
+// KERNEL_PERSIST = 8x8-pixel one-wave tiles pulled by persistent waves from an
+// atomic tile counter (SURVEY.md 7.5's refill at tile granularity, rm_params.kernel 4).
+enum KernelKind : int { KERNEL_TILE16 = 0, KERNEL_TILE8 = 1, KERNEL_TILE16X4 = 2, KERNEL_PERSIST = 3 };
 template <int K> struct Tiling;
 template <> struct Tiling<KERNEL_TILE16> { static constexpr int TW = 16, TH = 16, WPB = 4, LW = 8; };
 template <> struct Tiling<KERNEL_TILE8> { static constexpr int TW = 8, TH = 8, WPB = 1, LW = 8; };
 template <> struct Tiling<KERNEL_TILE16X4> { static constexpr int TW = 16, TH = 4, WPB = 1, LW = 16; };
+template <> struct Tiling<KERNEL_PERSIST> : Tiling<KERNEL_TILE8> {};
 
 // The body of a render launch: one lane per pixel of the workgroup's tile.
 // OUT = float4 (gl_FragColor) or uint32_t (RGBA8, packed in the epilogue, so
 // the displayed frame costs 4 B/px of HBM instead of 16 + 20 for a pack
 // pass).  COUNT: instrumented build, ray-steps and FLOP summed per wave into
 // evals[0..1].
+// (bx, by): the tile's position in dispatch order on a gx-wide tile grid
+// (blockIdx for the hardware-dispatched kernels).
 template <int SC, bool COUNT, int K, typename OUT>
-__device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict__ out,
-                                            unsigned long long* __restrict__ evals) {
+__device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restrict__ out,
+                                               unsigned long long* __restrict__ evals, int bx, int by, int gx) {
     using T = Tiling<K>;
     const uint64_t t_start = T::WPB == 1 && F.tile_cost ? clock64() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int bx = blockIdx.x, by = blockIdx.y;
     // scene T: the first lat_tiles workgroups of an ordered launch are its
     // costliest tiles, whose lone waves end the launch; they render with one
     // fold exit test instead of three (fewer branches, more VALU: C4 share and
     // C2 tails -16..19 %, a whole C3 frame +5 % if every tile did)
-    const bool lat = T::WPB == 1 && SC == SCENE_T && F.tile_order && (int)(by * gridDim.x + bx) < F.lat_tiles;
+    const bool lat = T::WPB == 1 && SC == SCENE_T && F.tile_order && by * gx + bx < F.lat_tiles;
     if (F.tile_order) {  // dispatch order != tile order (costliest tiles first, rm_set_tile_order)
-        const uint32_t t = F.tile_order[by * gridDim.x + bx];
-        bx = t % gridDim.x;
-        by = t / gridDim.x;
+        const uint32_t t = F.tile_order[by * gx + bx];
+        bx = t % gx;
+        by = t / gx;
     }
     const int x = bx * T::TW + (w & 1) * 8 + (lane % T::LW);
     const int j = by * T::TH + (w >> 1) * 8 + (lane / T::LW);
@@ -615,7 +629,7 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
         const int y = shard_row(F, F.row0 + j);
         float tcx, tcy;
         V3 ro, rd;
-        camera_ray(F, x, y, tcx, tcy, ro, rd);
+        camera_ray<FastMath<SC>::value>(F, x, y, tcx, tcy, ro, rd);
         const float vig = vignette<FastMath<SC>::value>(tcx, tcy);
         V3 c;
         if constexpr (SC == SCENE_T) {
@@ -630,7 +644,7 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
     }
     if (T::WPB == 1 && F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
         const uint64_t dt = clock64() - t_start;
-        F.tile_cost[by * gridDim.x + bx] = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;
+        F.tile_cost[by * gx + bx] = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;
     }
     if constexpr (COUNT) {
         if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;
@@ -639,6 +653,48 @@ __device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict
             atomicAdd(&evals[0], (unsigned long long)se);
             atomicAdd(&evals[1], (unsigned long long)sf);
         }
+    }
+}
+
+template <int SC, bool COUNT, int K, typename OUT>
+__device__ __forceinline__ void render_tile(const FrameConst& F, OUT* __restrict__ out,
+                                            unsigned long long* __restrict__ evals) {
+    render_tile_at<SC, COUNT, K, OUT>(F, out, evals, blockIdx.x, blockIdx.y, gridDim.x);
+}
+
+// Persistent waves (KERNEL_PERSIST): the dispatch ordinals k of the launch's
+// tiles are dealt to the 8 XCDs (k = x + 8 j on XCD x = blockIdx.x % 8, the
+// dispatcher's round robin), each XCD's waves pulling j from a counter of
+// their own (F.persist[kPersistStride * x]: device-scope atomics on one address
+// from all XCDs serialize), the next j fetched before the current tile renders
+// (the atomic's latency hides behind the tile).  Tile k renders as the
+// hardware-dispatched kernel renders workgroup k (same tile order, latency
+// tiles, tile durations), so pixels are identical.  The last wave to leave
+// (counter 8 counts them) resets the counters for the next launch that uses
+// them; no wave waits for another.
+constexpr int kPersistStride = 32;  // uint32 words between counters (128 B lines)
+constexpr int kPersistWords = 9 * kPersistStride;
+template <int SC, bool COUNT, typename OUT>
+__device__ __forceinline__ void render_persistent(const FrameConst& F, OUT* __restrict__ out,
+                                                  unsigned long long* __restrict__ evals, int gx, int ntiles) {
+    const int xcd = blockIdx.x & 7;
+    uint32_t* ctr = F.persist + kPersistStride * xcd;
+    const int nj = (ntiles - xcd + 7) >> 3;  // ordinals xcd, xcd + 8, ... below ntiles
+    auto ticket = [&]() {
+        int j = 0;
+        if (threadIdx.x == 0) j = (int)atomicAdd(ctr, 1u);
+        return __builtin_amdgcn_readfirstlane(j);
+    };
+    for (int j = ticket(); j < nj;) {
+        const int jn = ticket();
+        const int k = xcd + 8 * j;
+        render_tile_at<SC, COUNT, KERNEL_PERSIST, OUT>(F, out, evals, k % gx, k / gx, gx);
+        j = jn;
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(F.persist + 8 * kPersistStride, 1u) == gridDim.x - 1)
+            for (int x = 0; x < 9; x++) atomicExch(F.persist + kPersistStride * x, 0u);
     }
 }
 

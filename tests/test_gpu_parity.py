@@ -258,7 +258,7 @@ def test_fused_rgba8_epilogue_bit_exact(R, torch_cuda, scene):
     W, H, band, n = 77, 45, 4, 3
     full, sf = R.render(W, H, stats=True)
     packed = R.pack_rgba8(full)
-    for k in ("tile8", "tile16", "tile16x4"):
+    for k in ("tile8", "tile16", "tile16x4", "persist"):
         R.set_params(kernel=k)
         a, sa = R.render_rgba8(W, H, stats=True)
         assert torch.equal(a, packed), k
@@ -701,3 +701,29 @@ def test_latency_tiles_keep_pixels(R, torch_cuda):
     a, sa = R.render_rgba8(W, H, stats=True)
     assert torch.equal(a, ref) and sa["evals"] == st["evals"]
     R.set_params(count_evals=0)
+
+
+@pytest.mark.parametrize("scene", ["T", "O"])
+def test_persistent_waves_equal_hardware_dispatch(R, torch_cuda, scene):
+    """KERNEL_PERSIST (persistent waves pulling tiles from an atomic counter):
+    the frame of the hardware-dispatched kernel bit for bit, over repeated
+    launches (the counters reset themselves), with the adaptive order, on two
+    streams, and for shards whose tile count is below the resident-wave count."""
+    torch = torch_cuda
+    setup(R, scene, POSES["P1"], 128)
+    R.set_params(count_evals=0, kernel="tile8")
+    W, H = 200, 136
+    ref = R.render_rgba8(W, H)
+    band = R.render_band_rgba8(W, H, 8, 3, 1)
+    R.set_params(kernel="persist")
+    s2 = torch.cuda.Stream()
+    for i in range(8):
+        if i % 2:
+            R.set_stream(s2)
+        a = R.render_rgba8(W, H)
+        b = R.render_band_rgba8(W, H, 8, 3, 1)
+        R.set_stream(None)
+        torch.cuda.synchronize()
+        assert torch.equal(a, ref), i
+        assert torch.equal(b, band), i
+    R.set_params(kernel="auto")

@@ -18,7 +18,7 @@ CONFIGS = [  # name, scene, W, H, steps, pose, band, nshards, shard
 ]
 
 CHILD = r'''
-import json, sys, time, torch
+import json, os, sys, time, torch
 sys.path.insert(0, ".")
 import raymarching_amd as rm
 cfgs = json.loads(sys.argv[1])
@@ -28,7 +28,8 @@ for (name, scene, W, H, steps, pose, band, n, shard), sched in [(c, s) for c in 
     r.load_scene(rm.SCENE_FILES[scene])
     r.set_uniform("u_resolution", W, H)
     r.set_pose(p["pos"], p["mouse"], p["time"])
-    r.set_params(max_steps=steps, shadow_max_steps=0, count_evals=1, schedule=sched)
+    r.set_params(max_steps=steps, shadow_max_steps=0, count_evals=1, schedule=sched,
+                 kernel=os.environ.get("RM_KERNEL", "auto"))
     rows = rm.shard_rows(H, band, n, shard)
     out = torch.empty((rows, W), dtype=torch.int32, device="cuda")
     _, st = r.render_band_rgba8(W, H, band, n, shard, out=out, stats=True)
@@ -39,7 +40,7 @@ for (name, scene, W, H, steps, pose, band, n, shard), sched in [(c, s) for c in 
         r.render_band_rgba8(W, H, band, n, shard, out=out)
     torch.cuda.synchronize()
     ms = sorted(r.render_band_rgba8(W, H, band, n, shard, out=out, stats=True)[1]["kernel_ms"] for _ in range(15))
-    print(json.dumps(dict(lib=sys.argv[2], config=name, schedule=sched, kernel_ms=ms[len(ms) // 2], min_ms=ms[0],
+    print(json.dumps(dict(lib=sys.argv[2], kernel=os.environ.get("RM_KERNEL", "auto"), config=name, schedule=sched, kernel_ms=ms[len(ms) // 2], min_ms=ms[0],
                           ray_steps=evals, rate=evals / (ms[len(ms) // 2] / 1e3))), flush=True)
 '''
 
