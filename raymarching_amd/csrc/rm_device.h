@@ -201,7 +201,8 @@ __device__ __forceinline__ float sponge_box(V3 p) {
 // lanes past their exit point compute a fold that leaves d unchanged.  The
 // same VALU as a per-lane branch, without the two exec-mask SALU per test
 // (v_cmp to vcc + s_cbranch_vccz), and SALU issue is a co-bottleneck
-// (DESIGN.md 2.2).  The FLOP tally counts the folds a lane needs.
+// (DESIGN.md 2.2).  The FLOP tally counts the folds a lane needs, whatever NB
+// and the wave's other lanes make it compute.
 // NB: how many of the three folds keep their exit test.  A fold computed past
 // its exit point leaves d unchanged, so any NB gives the same distance: 3 (the
 // default) executes the fewest instructions, 1 the fewest branches and exec-mask
@@ -218,8 +219,8 @@ __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool 
     bool need = active;  // this lane's d can still change (fold m's test passed)
 #pragma unroll
     for (int m = 0; m < 3; m++) {
+        need = active && d < INV[m];  // (d only grows: implies the earlier tests)
         if (m < NB) {
-            need = active && d < INV[m];  // (d only grows: implies the earlier tests)
 #if RM_FOLD_UNIFORM
             if (__builtin_amdgcn_ballot_w64(need) == 0) return d;
 #else

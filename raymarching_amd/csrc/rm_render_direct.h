@@ -229,6 +229,8 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
 // The uncapped loop (the reference's, and the default) carries no step
 // counter: a uniform counter test merged into the lanes' exit mask costs 5
 // SALU per step, and SALU issue is a co-bottleneck of the kernel.
+// (Scene O's soft_shadow2 measured no gain from the same split: its kernel
+// spills at occupancy 8 and the second loop copy spilled more.)
 template <int NB = 3>
 __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                 Tally& cnt) {
