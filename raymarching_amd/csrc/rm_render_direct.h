@@ -152,6 +152,14 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
     return hit ? depth : depth >= ZFAR ? -1.0f : res;
 }
 
+// The soft-shadow loops compute P = 2h for the next step before the exit
+// test and pin it there (an empty asm): left free, the compiler sinks the add
+// into a "continue" block of its own, which costs 4 SALU and 2 branches per
+// step (C4 share 0.131 -> 0.119 ms, C2 P1 0.204 -> 0.188, scene O 4096^2
+// 2.97 -> 2.92; profiles/r02/shadow_p_pin_ab.jsonl).
+#ifndef RM_SHADOW_P_PIN
+#define RM_SHADOW_P_PIN 1
+#endif
 // common.frag:810-831, k = 4, for scenes O/OG: the probes step along the
 // world ray and its sponge-space image, and the candidate is kept squared as
 // in soft_shadow2_T below (the shadow factor is smooth in its roundings).
@@ -184,6 +192,9 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
         num = upd ? cn : num;
         den = upd ? cd : den;
         P = h + h;
+#if RM_SHADOW_P_PIN
+        asm volatile("" : "+v"(P));  // keep P's add in the step (not in a continue block of its own)
+#endif
         t += h * 0.1f + 0.001f;  // the reference's roundings: the step count is part of parity
         if ((h < 0.001f) | !(t < maxt) | (it >= F.shadow_max_steps)) break;
     }
@@ -218,6 +229,9 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
         num = upd ? cn : num;
         den = upd ? cd : den;
         P = h + h;
+#if RM_SHADOW_P_PIN
+        asm volatile("" : "+v"(P));  // keep P's add in the step (not in a continue block of its own)
+#endif
         t = fmaf(h, 0.1f, t + 0.001f);
         if ((h < 0.001f) | !(t < maxt) | (CAP && it >= F.shadow_max_steps)) break;
     }
