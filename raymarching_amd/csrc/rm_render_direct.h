@@ -97,9 +97,6 @@ __device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt,
     return mnormalize<SC>(g);
 }
 
-#ifndef RM_SPAN_UNIFORM
-#define RM_SPAN_UNIFORM 0
-#endif
 // common.frag:879-901. Returns dist (depth on hit, -1 on miss, last SDF value
 // on step exhaustion) and the point whose SdResult is returned.  One exit
 // test per step; at a hit depth is left as it was, so the hit flag and depth
@@ -114,26 +111,6 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
         const float ia = plane_rate(rd);
         float t_plane = 0.0f, last = 0.0f;
         for (int i = 0; i < F.max_steps; i++) {
-#if RM_SPAN_UNIFORM
-            // wave-uniform: a lane inside its span gets the plane's value from
-            // the full evaluation too (that is what the span certifies, bit for
-            // bit), so a mixed wave runs the full path alone, with no exec-mask
-            // split; the span is then re-certified from this point
-            const bool span = depth < t_plane;
-            if (__builtin_amdgcn_ballot_w64(!span) == 0) {
-                res = ro.y + rd.y * depth;
-                cnt.evals++;
-                cnt.flop += 2;
-            } else {
-                V3 q = ro + rd * depth;
-                float slack;
-                Tally tl;
-                res = scene_dist_O<true>(q, sponge_space<true>(F, q), tl, slack);
-                t_plane = depth + slack * ia;
-                cnt.evals++;
-                cnt.flop += span ? 2 : FL_TRANSFORM + tl.flop;
-            }
-#else
             if (depth < t_plane) {
                 res = ro.y + rd.y * depth;
                 cnt.evals++;
@@ -145,7 +122,6 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
                 res = scene_dist_O<true>(q, sponge_space<true>(F, q), cnt, slack);
                 t_plane = depth + slack * ia;
             }
-#endif
             last = depth;
             if (INSIDE) {
                 hit = -res < 0.001f * depth;
@@ -198,21 +174,6 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
     for (int it = 1; it == 1 ? t < maxt : true; it++) {
         if constexpr (SC == SCENE_PLUGIN) {
             h = dist_probe<SC>(F, at(w, t), cnt);
-#if RM_SPAN_UNIFORM
-        } else if (__builtin_amdgcn_ballot_w64(!(t < t_plane)) == 0) {  // (wave-uniform: cast_ray_d)
-            h = fmaf(w.d.y, t, w.o.y);  // at(w, t).y
-            cnt.evals++;
-            cnt.flop += 2;
-        } else {
-            float slack;
-            Tally tl;
-            const bool span = t < t_plane;
-            h = scene_dist_O<false>(at(w, t), at(s, t), tl, slack);
-            t_plane = t + slack * ia;
-            cnt.evals++;
-            cnt.flop += span ? 2 : FL_LINRAY + tl.flop;
-        }
-#else
         } else if (t < t_plane) {
             h = fmaf(w.d.y, t, w.o.y);  // at(w, t).y
             cnt.evals++;
@@ -223,7 +184,6 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
             h = scene_dist_O<false>(at(w, t), at(s, t), cnt, slack);
             t_plane = t + slack * ia;
         }
-#endif
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
         float D = it == 1 ? t : fmaf(t, P, -h2);
