@@ -67,6 +67,9 @@ def lib(fast: bool = False) -> ctypes.CDLL:
         L.oracle_render_rows.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, i32p,
                                          ctypes.c_int, f32p, u32p]
         L.oracle_render_rows.restype = ctypes.c_int
+        L.oracle_render_pixels.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, i32p, ctypes.c_int, f32p,
+                                           u32p]
+        L.oracle_render_pixels.restype = ctypes.c_int
         for fn in ("oracle_scene_dist", "oracle_normal"):
             getattr(L, fn).argtypes = [ctypes.c_int, up, f32p, ctypes.c_int, f32p]
             getattr(L, fn).restype = ctypes.c_int
@@ -165,6 +168,20 @@ def render_rows(scene: str, W: int, H: int, rows, fast=False, **kw):
                                       len(rows), _p(out, ctypes.c_float), _p(ev, ctypes.c_uint32))
     if rc:
         raise ValueError(f"oracle_render_rows failed rc={rc}")
+    return out, ev
+
+
+def render_pixels(scene: str, W: int, H: int, xs, ys, fast=False, **kw):
+    """Pixels (xs[i], ys[i]) of a W x H frame -> (rgba f32 [n, 4], evals u32 [n])."""
+    xy = np.ascontiguousarray(np.stack([np.asarray(xs, np.int32).ravel(), np.asarray(ys, np.int32).ravel()], -1))
+    n = len(xy)
+    u = uniforms(W, H, **kw)
+    out = np.zeros((n, 4), np.float32)
+    ev = np.zeros(n, np.uint32)
+    rc = lib(fast).oracle_render_pixels(SCENES[scene], ctypes.byref(u), W, H, _p(xy, ctypes.c_int32), n,
+                                        _p(out, ctypes.c_float), _p(ev, ctypes.c_uint32))
+    if rc:
+        raise ValueError(f"oracle_render_pixels failed rc={rc}")
     return out, ev
 
 

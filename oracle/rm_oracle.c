@@ -818,6 +818,27 @@ int oracle_render_rows(int scene, const oracle_uniforms *u, int W, int H, const 
     return 0;
 }
 
+/* Render an explicit list of pixels (x, y) = (xy[2i], xy[2i+1]) of a W x H
+ * frame: out n*4 f32, evals (optional) n u32.  Full-size parity samples that
+ * are not whole rows (column-strided blocks). */
+int oracle_render_pixels(int scene, const oracle_uniforms *u, int W, int H, const int32_t *xy, int n, float *out,
+                         uint32_t *evals) {
+    if (!u || !out || !xy || W <= 0 || H <= 0 || n < 0) return 1;
+    if (scene < SCENE_S0 || scene > SCENE_OG) return 2;
+    for (int i = 0; i < n; i++)
+        if (xy[2 * i] < 0 || xy[2 * i] >= W || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= H) return 1;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int i = 0; i < n; i++) {
+        Ctx C;
+        uint64_t cnt = 0;
+        init_ctx(&C, scene, u);
+        C.evals = &cnt;
+        shade_pixel(&C, W, H, xy[2 * i], xy[2 * i + 1], out + (size_t)i * 4);
+        if (evals) evals[i] = (uint32_t)cnt;
+    }
+    return 0;
+}
+
 /* Per-pixel sceneSDF segments (analysis aid): seg = nrows*W*MAX_SEG*2 u16,
  * nseg = nrows*W u8. */
 int oracle_render_segments(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, uint16_t *seg,

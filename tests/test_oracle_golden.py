@@ -52,7 +52,8 @@ def test_oracle_matches_reference_glsl(path):
                             max_steps=m["max_steps"])
     assert img.shape == rgba.shape
     ok = defined(img)
-    assert ok.mean() >= (0.3 if m["pose"] == "P7" else 1.0)
+    # OG at P7 (camera inside the glass): 66 % of the pixels are defined
+    assert ok.mean() >= (0.6 if m["pose"] == "P7" else 1.0)
     s = assert_parity(m["scene"], img[ok], rgba[ok], label=os.path.basename(path))
     assert s["max"] <= MAX_ABS, s
     # the per-pixel step counts (sceneSDF calls) of the reference GLSL run

@@ -141,3 +141,21 @@ def test_oracle_under_address_and_undefined_behaviour_sanitizers():
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "selftest ok" in r.stdout
+
+
+def test_render_pixels_equals_rows():
+    """oracle.render_pixels (column-strided full-size samples) renders a pixel
+    exactly as render_rows does: colour and ray-step count."""
+    import numpy as np
+
+    from raymarching_amd import POSES
+    kw = {k: POSES["P2"][k] for k in ("pos", "mouse", "time")}
+    rows = np.array([7, 100], np.int32)
+    o, ev = oracle.render_rows("O", 320, 200, rows, max_steps=128, **kw)
+    xs = np.tile(np.arange(320), 2)
+    ys = np.repeat(rows, 320)
+    o2, ev2 = oracle.render_pixels("O", 320, 200, xs, ys, max_steps=128, **kw)
+    assert np.array_equal(o.reshape(-1, 4), o2)
+    assert np.array_equal(ev.ravel(), ev2)
+    with pytest.raises(ValueError):
+        oracle.render_pixels("O", 320, 200, [320], [0])

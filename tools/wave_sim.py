@@ -111,3 +111,72 @@ def band_main(scene, W, steps, pn, row0, nrows):
     for K in (64, 256, 1024):
         res[f"compact{K}"] = compact_eff(tot, K)
     print(scene, W, {k: round(v, 3) if isinstance(v, float) else v for k, v in res.items()}, flush=True)
+
+
+# ---------------------------------------------------------------- per phase
+PHASE_NAMES = {"O": ["march", "normal", "AO", "shadow", "SSS", "refl.march", "refl.normal", "refl.AO",
+                     "refl.shadow", "refl.SSS"],
+               "T": ["march", "normal", "refl.march", "AO", "shadow"], "S0": ["march", "normal"]}
+
+
+def aligned_np(seg, ns, tmpl):
+    """aligned() vectorized: [..., len(tmpl)] counts per code position."""
+    P = len(tmpl)
+    nxt = np.full((P + 1, 8), P, np.int64)  # next position >= k holding phase ph
+    for k in range(P - 1, -1, -1):
+        nxt[k] = nxt[k + 1]
+        nxt[k, tmpl[k]] = k
+    shp = ns.shape
+    seg = seg.reshape(-1, seg.shape[-2], 2)
+    ns = ns.reshape(-1)
+    out = np.zeros((len(ns), P + 1), np.int64)
+    k = np.zeros(len(ns), np.int64)
+    rows = np.arange(len(ns))
+    for i in range(seg.shape[1]):
+        live = i < ns
+        ph = seg[:, i, 0].astype(np.int64)
+        c = seg[:, i, 1].astype(np.int64)
+        pos = nxt[np.minimum(k, P), ph]
+        pos = np.where(live, pos, P)
+        np.add.at(out, (rows, pos), np.where(live, c, 0))
+        k = np.where(live & (pos < P), pos + 1, k)
+    return out[:, :P].reshape(*shp, P)
+
+
+def phase_report(scene, W, steps, pn, bands, rows_per_band=64):
+    """Lane utilization per code position of the one-wave 8x8 tiles, over
+    `bands` row bands spread over a W x W frame: useful lane-steps / (64 x the
+    wave's longest lane), and the lanes that reach each phase among the waves
+    that run it (the shading code of that phase runs at that utilization)."""
+    L = oracle.lib()
+    pose = POSES[pn]
+    u = oracle.uniforms(W, W, pos=pose["pos"], mouse=pose["mouse"], time=pose["time"], max_steps=steps)
+    L.oracle_render_segments.argtypes = [ctypes.c_int, ctypes.POINTER(oracle.OracleUniforms), ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    tmpl = TEMPLATES[scene]
+    acc = []
+    for b in range(bands):
+        row0 = (W // bands * b + W // (2 * bands)) // 8 * 8
+        seg = np.zeros((rows_per_band, W, 24, 2), np.uint16)
+        ns = np.zeros((rows_per_band, W), np.uint8)
+        L.oracle_render_segments(oracle.SCENES[scene], ctypes.byref(u), W, W, row0, rows_per_band, seg.ctypes.data,
+                                 ns.ctypes.data)
+        acc.append(tiles(aligned_np(seg, ns, tmpl)))
+    w = np.concatenate(acc)  # [nwaves, 64, P]
+    useful = w.sum(axis=(0, 1))
+    cost = w.max(axis=1).sum(axis=0) * 64
+    reach = (w > 0)
+    waves_run = reach.any(axis=1)  # [nwaves, P]
+    lanes_reach = reach.sum(axis=1)
+    names = PHASE_NAMES.get(scene, [str(k) for k in range(len(tmpl))])
+    out = {"scene": scene, "W": W, "steps": steps, "pose": pn, "waves": int(len(w)),
+           "evals/px": round(float(w.sum() / (len(w) * 64)), 2), "direct": round(float(useful.sum() / cost.sum()), 4),
+           "phases": {}}
+    for k, nm in enumerate(names):
+        nrun = int(waves_run[:, k].sum())
+        out["phases"][nm] = {
+            "evals_share": round(float(useful[k] / useful.sum()), 4),
+            "step_util": round(float(useful[k] / max(cost[k], 1)), 4),
+            "lane_util": round(float(lanes_reach[:, k][waves_run[:, k]].sum() / max(64 * nrun, 1)), 4),
+            "waves_run": round(nrun / len(w), 4)}
+    return out
