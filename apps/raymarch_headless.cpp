@@ -12,6 +12,12 @@
 // Usage: raymarch_headless [--scene output_shader.frag] [--w 1600] [--h 900]
 //          [--frames 60] [--script WWWWDD..] [--mouse 3,0] [--time-freeze]
 //          [--steps 128] [--ppm out.ppm] [--gpus N] [--band 16] [--accumulate]
+//          [--format rgba8|float] [--stats] [--warmup N]
+// Frames are drawn into the RGBA8 target the reference renders into
+// (--format float: RGBA32F) and queued without a host synchronization per
+// frame; --stats times each frame's kernel (HIP events, which waits for every
+// frame) and reports kernel_ms_per_frame.  fps_wall counts the frames after
+// --warmup (untimed) frames, up to the completion of the last one.
 // --gpus N renders each frame's row bands on GPUs 0..N-1 and gathers them over
 // RCCL to GPU 0 (rm::ShardedRenderTexture -> rm_render_sharded_all); --sharded
 // takes that path with one GPU too.
@@ -31,7 +37,8 @@ int main(int argc, char** argv) {
     std::string scene = "output_shader.frag", script, ppm;
     int w = 1600, h = 900, frames = 60, steps = 128, gpus = 1, band = 16;
     int mdx = 0, mdy = 0;
-    bool time_freeze = false, sharded = false, accumulate = false;
+    bool time_freeze = false, sharded = false, accumulate = false, stats = false, fmt_float = false;
+    int warmup = 0;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() { return i + 1 < argc ? std::string(argv[++i]) : std::string(); };
@@ -47,6 +54,16 @@ int main(int argc, char** argv) {
         else if (a == "--time-freeze") time_freeze = true;
         else if (a == "--sharded") sharded = true;
         else if (a == "--accumulate") accumulate = true;
+        else if (a == "--stats") stats = true;
+        else if (a == "--warmup") warmup = std::atoi(next().c_str());
+        else if (a == "--format") {
+            const std::string f = next();
+            if (f != "rgba8" && f != "float") {
+                std::fprintf(stderr, "--format rgba8|float\n");
+                return 2;
+            }
+            fmt_float = f == "float";
+        }
         else if (a == "--mouse") std::sscanf(next().c_str(), "%d,%d", &mdx, &mdy);
         else {
             std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -90,7 +107,8 @@ int main(int argc, char** argv) {
     };
     rm::RenderTexture outputTexture;
     rm::ShardedRenderTexture shardedTexture;
-    if (!sharded ? !outputTexture.create(w, h) : !shardedTexture.create(w, h, all, band)) {
+    if (!sharded ? !outputTexture.create(w, h, fmt_float ? rm::RenderTexture::RGBA32F : rm::RenderTexture::RGBA8)
+                 : !shardedTexture.create(w, h, all, band)) {
         std::fprintf(stderr, "cannot allocate the %dx%d target on %d GPU(s): %s\n", w, h, gpus,
                      shader.lastError().c_str());
         return 1;
@@ -99,8 +117,13 @@ int main(int argc, char** argv) {
     std::mt19937 e2(20261015);
     std::uniform_real_distribution<float> dist(0.0f, 1.0f);
     auto t0 = std::chrono::steady_clock::now();
+    auto t_timed = t0;
     double kernel_ms = 0.0;
-    for (int f = 0; f < frames; f++) {
+    for (int f = 0; f < warmup + frames; f++) {
+        if (f == warmup) {  // the timed frames start when the warm-up frames are done
+            if (rm_synchronize(shader.ctx()) != RM_OK) return 1;
+            t_timed = std::chrono::steady_clock::now();
+        }
         bool wasd[6] = {false, false, false, false, false, false};
         char k = f < (int)script.size() ? script[f] : '.';
         const char keys[] = "WASDUN";
@@ -131,25 +154,29 @@ int main(int argc, char** argv) {
         setAll("u_seed1", seed1);
         setAll("u_seed2", seed2);
         std::vector<rm_stats> st(gpus);
+        rm_stats* stp = stats ? st.data() : nullptr;
         // --accumulate: the pass reads u_sample/u_sample_part/u_seed1 (progressive
         // supersampling while the camera is still; one GPU)
-        const bool drawn = sharded      ? shardedTexture.draw(st.data())
-                           : accumulate ? outputTexture.drawAccumulate(shader, st.data())
-                                        : outputTexture.draw(shader, st.data());
+        const bool drawn = sharded      ? shardedTexture.draw(stp)
+                           : accumulate ? outputTexture.drawAccumulate(shader, stp)
+                                        : outputTexture.draw(shader, stp);
         if (!drawn) {
             std::fprintf(stderr, "draw failed: %s\n", shader.lastError().c_str());
             return 1;
         }
         float slowest = 0.0f;
         for (const rm_stats& x : st) slowest = x.kernel_ms > slowest ? x.kernel_ms : slowest;
-        kernel_ms += slowest;
+        if (f >= warmup) kernel_ms += slowest;
         framesStill++;
     }
-    double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::printf("{\"frames\": %d, \"w\": %d, \"h\": %d, \"gpus\": %d, \"scene\": \"%s\", "
-                "\"kernel_ms_per_frame\": %.4f, \"fps_wall\": %.2f, \"pos\": [%.4f, %.4f, %.4f]}\n",
-                frames, w, h, gpus, scene.c_str(), frames ? kernel_ms / frames : 0.0, frames / wall, pos.x, pos.y,
-                pos.z);
+    for (rm::Shader* s : all)
+        if (rm_synchronize(s->ctx()) != RM_OK) return 1;
+    double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_timed).count();
+    std::printf("{\"frames\": %d, \"warmup\": %d, \"w\": %d, \"h\": %d, \"gpus\": %d, \"scene\": \"%s\", "
+                "\"format\": \"%s\", \"fps_wall\": %.2f, ",
+                frames, warmup, w, h, gpus, scene.c_str(), sharded || !fmt_float ? "rgba8" : "float", frames / wall);
+    if (stats) std::printf("\"kernel_ms_per_frame\": %.4f, ", frames ? kernel_ms / frames : 0.0);
+    std::printf("\"pos\": [%.4f, %.4f, %.4f]}\n", pos.x, pos.y, pos.z);
     if (!ppm.empty()) {
         std::vector<uint32_t> px;
         if (!sharded ? !outputTexture.copyToHostRGBA8(shader, px) : !shardedTexture.copyToHostRGBA8(px)) return 1;

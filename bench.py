@@ -21,8 +21,16 @@ the timed region (max over ranks).  The per-frame step count comes from one
 instrumented run of the same kernel (count_evals) before timing; the timed
 runs are uninstrumented.
 
+--walk measures under the reference's operating condition instead of a still
+camera: every frame moves the camera one step forward as main.cpp does with W
+held (pos += dir * 0.1 along the view-rotated axes, main.cpp:153-171) and
+advances u_time by the 60 Hz frame interval (main.cpp:30,190-191), which
+rotates the sponge.  The warm-up frames walk up to the start pose, the timed
+frames walk on from it (deterministic poses; their ray-steps are counted by an
+instrumented pass over the same poses before timing).
+
 Usage: python bench.py [--gpus N --steps K --warmup W] [--scene T|O|S0]
-       [--size 4096] [--max-steps 256] [--pose P0] [--band 16]
+       [--size 4096] [--max-steps 256] [--pose P0] [--band 16] [--walk]
        [--fmt rgba8|float4] [--kernel auto|tile16|tile8] [--cpu-seconds 12]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
@@ -66,6 +74,10 @@ def parse():
                     help="tile dispatch order: costliest tiles of the previous frame first, or row-major")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
+    ap.add_argument("--walk", action="store_true",
+                    help="moving camera and advancing u_time (main.cpp's W key at 60 Hz) instead of a still pose")
+    ap.add_argument("--walk-speed", type=float, default=0.1, help="camera step per frame (main.cpp:21 speed)")
+    ap.add_argument("--walk-dt", type=float, default=1.0 / 60.0, help="u_time step per frame (main.cpp:30)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(HERE, "profiles", "pmc_counters.json"),
                     help="per-workload rocprofv3 PMC counters (profiles/): executed FP32 ops for "
@@ -84,6 +96,21 @@ def _config_id(scene, W, H, max_steps, world):
     if scene == "O" and (W, H, max_steps) == (8192, 8192, 512):
         return "C5"
     return "custom"
+
+
+def walk_pose(pose, i, speed, dt):
+    """Frame i of a walk from `pose` (i < 0: the frames before it): main.cpp's
+    camera step with W held, pos += dir * speed with dir = (0, 0, -1) rotated by
+    the pose's mouse angles (YZ by -my, then XZ by mx, main.cpp:155-171), and
+    u_time advanced by dt per frame (main.cpp:190-191)."""
+    import math
+
+    mx, my = pose["mouse"]
+    dty, dtz = math.sin(-my), -math.cos(-my)        # rotate YZ: dir = (0, 0, -1)
+    dx, dz = -dtz * math.sin(mx), dtz * math.cos(mx)  # rotate XZ
+    px, py, pz = pose["pos"]
+    return dict(pos=(px + dx * speed * i, py + dty * speed * i, pz + dz * speed * i), mouse=pose["mouse"],
+                time=pose["time"] + dt * i)
 
 
 def cpu_baseline(args, pose, W, H, target_s):
@@ -204,9 +231,17 @@ def roofline(pmc, flop_tally, evals, ref_flop_per_step, kern_ms, out_bytes):
     evaluated).  VALU/SALU issue fractions beside it."""
     t = kern_ms / 1e3
     keys = ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32")
+    slots, lane_frac = None, None
     if all(k in pmc for k in keys):
-        flop = 64 * (pmc[keys[0]] + pmc[keys[1]] + pmc[keys[2]] + 2 * pmc[keys[3]])
-        src = f"PMC executed FP32 ops ({pmc.get('source')}): 64 x (ADD + MUL + TRANS + 2 FMA)"
+        # issued FP32 lane slots (64 per wave-instruction), scaled by the mean
+        # active-lane fraction of VALU instructions (exec mask): the FLOP that
+        # active lanes did
+        slots = 64 * (pmc[keys[0]] + pmc[keys[1]] + pmc[keys[2]] + 2 * pmc[keys[3]])
+        lane_frac = pmc.get("active_lane_frac")
+        flop = slots * (lane_frac or 1.0)
+        src = (f"PMC executed FP32 ops ({pmc.get('source')}): 64 x (ADD + MUL + TRANS + 2 FMA)"
+               + (" x active-lane fraction SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)" if lane_frac else
+                  " (issued lane slots: no active-lane counter for this workload)"))
     else:
         flop = flop_tally
         src = "instrumented tally (no PMC counters for this workload in profiles/)"
@@ -215,6 +250,8 @@ def roofline(pmc, flop_tally, evals, ref_flop_per_step, kern_ms, out_bytes):
         "bound": "valu", "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": ach / PEAK_FP32_TFLOPS, "traffic": pmc.get("hbm_bytes_per_launch"),
         "flop_per_launch": flop, "flop_source": src, "ray_steps_per_launch": evals,
+        "issued_lane_slot_flop_per_launch": slots, "active_lane_frac": lane_frac,
+        "issued_lane_slot_frac": None if slots is None else slots / t / 1e12 / PEAK_FP32_TFLOPS,
         "tally_flop_per_launch": flop_tally, "tally_tflops": flop_tally / t / 1e12,
         "reference_tally_flop_per_ray_step": ref_flop_per_step,
         "reference_equivalent_tflops": evals * ref_flop_per_step / t / 1e12,
@@ -269,9 +306,21 @@ def main():
     chunks = args.chunks if args.chunks is not None else 1
     fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks, streams=args.streams)
 
-    # instrumented run: ray-steps of this rank's rows, summed over ranks
+    def set_frame(i):  # walk: the pose of frame i (timed frames 0..K-1)
+        if args.walk:
+            p = walk_pose(pose, i, args.walk_speed, args.walk_dt)
+            r.set_pose(p["pos"], p["mouse"], p["time"])
+
+    # instrumented run: ray-steps of this rank's rows, summed over ranks (with
+    # --walk: per timed pose, their mean is the frame's count)
     r.set_params(count_evals=1)
-    _, st = fr.render_local(stats=True)
+    walk_evals = []
+    for i in range(args.steps if args.walk else 1):
+        set_frame(i)
+        _, st = fr.render_local(stats=True)
+        walk_evals.append(st["evals"])
+    if args.walk:
+        st = dict(st, evals=sum(walk_evals) / len(walk_evals))
     r.set_params(count_evals=0)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
     ev_rank = torch.tensor([st["evals"]], dtype=torch.float64, device=red_dev)
@@ -286,6 +335,7 @@ def main():
     # Every rank runs the same number of rounds (each frame holds a gather), so
     # whether to go on is agreed over all ranks after each round.
     t_spin = time.perf_counter()
+    set_frame(-args.warmup)
     while args.spinup > 0:
         for _ in range(8):
             fr.submit()
@@ -296,7 +346,8 @@ def main():
             dist.all_reduce(go, op=dist.ReduceOp.MIN)
         if go.item() == 0.0:
             break
-    for _ in range(args.warmup):
+    for i in range(-args.warmup, 0):
+        set_frame(i)
         fr.submit()
     fr.flush()
     torch.cuda.synchronize(dev)
@@ -309,6 +360,7 @@ def main():
            for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
+        set_frame(i)
         fr.submit(events=evs[i])  # frame i's gather overlaps frame i+1's render
     fr.flush()
     torch.cuda.synchronize(dev)
@@ -324,6 +376,7 @@ def main():
     # per-launch render-kernel duration (the roofline denominator): synchronous launches of this rank's
     # rows on the frames' stream, HIP events around the kernel alone (rm_stats.kernel_ms), after the
     # timed region
+    set_frame(args.steps - 1)
     launch = sorted(fr.render_local(stats=True)[1]["kernel_ms"] for _ in range(11)) if fr.nmine else [0.0]
     kern = launch[len(launch) // 2]
     kt = torch.tensor([kern], dtype=torch.float64, device=red_dev)
@@ -339,7 +392,9 @@ def main():
         pmc = {}
         try:
             pm = json.load(open(args.pmc))
-            key = f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}" + ("" if world == 1 else f"_n{world}")
+            # (a walk renders other poses than the still frame the counters were taken on)
+            key = (f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}" + ("" if world == 1 else f"_n{world}")
+                   + ("_walk" if args.walk else ""))
             pmc = pm.get(key, {})
         except (OSError, ValueError):
             pass
@@ -361,10 +416,16 @@ def main():
             "config": {
                 "workload": f"{_config_id(args.scene, W, H, args.max_steps, world)}: {W}x{H} scene {args.scene} "
                             f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
-                            f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0",
+                            f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0"
+                            + (f", walking (camera +{args.walk_speed}/frame forward, u_time +{args.walk_dt:.4f} s/frame)"
+                               if args.walk else ""),
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
                 "band": args.band, "fmt": args.fmt, "wire": fr.wire, "streams": len(fr.streams), "kernel": args.kernel, "chunks": chunks, "schedule": args.schedule,
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
+                "walk": None if not args.walk else {
+                    "speed": args.walk_speed, "dt": args.walk_dt, "frames": args.steps,
+                    "rank0_ray_steps_min": min(walk_evals), "rank0_ray_steps_max": max(walk_evals),
+                    "end_pose": walk_pose(pose, args.steps - 1, args.walk_speed, args.walk_dt)},
             },
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max, "frame_stream_ms": frame_stream_ms,
             "kernel_ms_note": "median per-launch duration of the render kernel (HIP events on its stream, "

@@ -9,7 +9,7 @@
 //   shader.setUniform("u_pos", sf::Vector3f)           shader.setUniform("u_pos", rm::Vec3{...})
 //   sf::RenderTexture t; t.create(w, h);               rm::RenderTexture t; t.create(w, h);
 //   t.draw(sprite, &shader);                           t.draw(shader);
-//   t.getTexture()                                     t.texture() (device RGBA32F) / t.copyToHost(...)
+//   t.getTexture()                                     t.textureRGBA8() (device RGBA8) / t.copyToHostRGBA8(...)
 //
 // Errors follow the reference: loadFromFile prints and returns false
 // (source/shader_loader.cpp:26-30); other calls return false and keep the
@@ -79,48 +79,73 @@ struct ShaderLoader {
     }
 };
 
-// A W x H RGBA32F render target resident in device memory (sf::RenderTexture).
+// A W x H render target resident in device memory (sf::RenderTexture).  RGBA8
+// by default, the format the reference's RenderTextures hold (main.cpp:34-50):
+// the kernel packs the pixel in its epilogue (rm_render_rgba8, 4 B/px of HBM);
+// RGBA32F keeps gl_FragColor unrounded (rm_render, 16 B/px).  A draw is
+// asynchronous on the shader's stream; copyToHostRGBA8 waits for it.
 class RenderTexture {
 public:
+    enum Format { RGBA8, RGBA32F };
+
     ~RenderTexture() { release(); }
-    bool create(int w, int h) {
+    bool create(int w, int h, Format fmt = RGBA8) {
         release();
         w_ = w;
         h_ = h;
-        return hipMalloc(&tex_, (size_t)w * h * 4 * sizeof(float)) == hipSuccess;
+        fmt_ = fmt;
+        return hipMalloc(&tex_, (size_t)w * h * (fmt == RGBA8 ? 4 : 16)) == hipSuccess;
     }
     // RenderTarget::draw(sprite, &shader) with the full-screen sprite (main.cpp:199,205)
     bool draw(Shader& shader, rm_stats* stats = nullptr) {
-        return tex_ && rm_render(shader.ctx(), w_, h_, tex_, stats) == RM_OK;
+        if (!tex_) return false;
+        return (fmt_ == RGBA8 ? rm_render_rgba8(shader.ctx(), w_, h_, static_cast<uint32_t*>(tex_), stats)
+                              : rm_render(shader.ctx(), w_, h_, static_cast<float*>(tex_), stats)) == RM_OK;
     }
     // The same draw reading the ping-pong plumbing (u_sample = this texture,
     // u_sample_part, u_seed1; main.cpp:192-207): progressive accumulation
-    // (rm_render_accumulate).  In place: each pixel reads only itself.
+    // (rm_render_accumulate[_rgba8]).  In place: each pixel reads only itself.
     bool drawAccumulate(Shader& shader, rm_stats* stats = nullptr) {
-        return tex_ && rm_render_accumulate(shader.ctx(), w_, h_, tex_, stats) == RM_OK;
+        if (!tex_) return false;
+        return (fmt_ == RGBA8 ? rm_render_accumulate_rgba8(shader.ctx(), w_, h_, static_cast<uint32_t*>(tex_), stats)
+                              : rm_render_accumulate(shader.ctx(), w_, h_, static_cast<float*>(tex_), stats)) ==
+               RM_OK;
     }
-    float* texture() { return tex_; }
+    Format format() const { return fmt_; }
+    // the device target: RGBA8 words (R in the low byte) or RGBA32F texels
+    uint32_t* textureRGBA8() { return fmt_ == RGBA8 ? static_cast<uint32_t*>(tex_) : nullptr; }
+    float* texture() { return fmt_ == RGBA32F ? static_cast<float*>(tex_) : nullptr; }
     int width() const { return w_; }
     int height() const { return h_; }
-    // RGBA8 (the reference target's format), row 0 first (looks up).
+    // RGBA8 (the reference target's format), row 0 first (looks up).  An
+    // RGBA32F target is packed into a device buffer kept for later calls.
     bool copyToHostRGBA8(Shader& shader, std::vector<uint32_t>& out) {
         out.resize((size_t)w_ * h_);
-        uint32_t* d = nullptr;
-        if (hipMalloc(&d, out.size() * sizeof(uint32_t)) != hipSuccess) return false;
-        bool ok = rm_pack_rgba8(shader.ctx(), (int64_t)out.size(), tex_, d) == RM_OK &&
-                  rm_synchronize(shader.ctx()) == RM_OK &&
-                  hipMemcpy(out.data(), d, out.size() * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess;
-        (void)hipFree(d);
-        return ok;
+        const uint32_t* src = textureRGBA8();
+        if (!src) {
+            if (!packed_ && hipMalloc(&packed_, out.size() * sizeof(uint32_t)) != hipSuccess) {
+                packed_ = nullptr;
+                return false;
+            }
+            if (rm_pack_rgba8(shader.ctx(), (int64_t)out.size(), static_cast<const float*>(tex_), packed_) != RM_OK)
+                return false;
+            src = packed_;
+        }
+        return rm_synchronize(shader.ctx()) == RM_OK &&
+               hipMemcpy(out.data(), src, out.size() * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess;
     }
 
 private:
     void release() {
         if (tex_) (void)hipFree(tex_);
+        if (packed_) (void)hipFree(packed_);
         tex_ = nullptr;
+        packed_ = nullptr;
     }
-    float* tex_ = nullptr;
+    void* tex_ = nullptr;
+    uint32_t* packed_ = nullptr;
     int w_ = 0, h_ = 0;
+    Format fmt_ = RGBA8;
 };
 
 // The multi-GPU form of RenderTexture::draw: a W x H RGBA8 frame whose row

@@ -39,8 +39,10 @@ struct rm_ctx {
     float pos[3] = {0.0f, 0.0f, 0.0f};
     float mouse[2] = {0.0f, 0.0f};
     float time = 0.0f;
-    uint32_t *persist = nullptr;  // KERNEL_PERSIST: kPersistSlots pairs of self-resetting tile counters
-    uint64_t persist_k = 0;       // launches that used them (slot = persist_k % kPersistSlots)
+    // KERNEL_PERSIST: one block of self-resetting tile counters per stream the
+    // context launched on (launches on one stream run one after another, so a
+    // block is never shared by two launches in flight)
+    std::vector<std::pair<hipStream_t, uint32_t *>> persist;
     float sample_part = 1.0f;  // u_sample_part, u_seed1, u_seed2: read by rm_render_accumulate*
     float seed1[2] = {0.0f, 0.0f}, seed2[2] = {0.0f, 0.0f};
     rm_params params = {128, 0, 0, 0, 1};
@@ -70,6 +72,7 @@ struct rm_ctx {
         uint64_t k = 0;            // launches so far
         uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256])
         hipEvent_t rendered = nullptr, sorted[2] = {nullptr, nullptr};
+        hipEvent_t last = nullptr;  // recorded after every launch that reads or writes buf
         uint64_t used = 0;
     };
     Sched sched[8];
@@ -264,8 +267,6 @@ int lat_tiles() {
 // the duration stores, the sort and the cross-stream events run on one launch
 // in four (C3 frame 0.683 -> 0.672 ms).  RM_SCHED_PERIOD
 // overrides it (1 = re-sort after every launch).
-constexpr int kPersistSlots = 8;
-
 int sched_period() {
     static const int n = [] {
         const char *e = std::getenv("RM_SCHED_PERIOD");
@@ -333,15 +334,17 @@ int pick_kernel(const rm_ctx *c) {
     return rm::KERNEL_TILE8;  // 0 auto, 2: measured fastest on every config
 }
 
-// Free an adaptive-order entry once nothing still reads or writes its buffers.
+// Free an adaptive-order entry once nothing still reads or writes its buffers:
+// its last launch (an event: the stream it ran on may belong to the caller and
+// be gone by now) and the context's own sort stream.
 hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
     hipError_t r = hipSuccess;
     if (e.buf) {
-        r = hipStreamSynchronize(e.stream);
+        if (e.last) r = hipEventSynchronize(e.last);
         if (r == hipSuccess && ctx->side) r = hipStreamSynchronize(ctx->side);
         (void)hipFree(e.buf);
     }
-    for (hipEvent_t ev : {e.rendered, e.sorted[0], e.sorted[1]})
+    for (hipEvent_t ev : {e.rendered, e.sorted[0], e.sorted[1], e.last})
         if (ev) (void)hipEventDestroy(ev);
     e = rm_ctx::Sched();
     return r;
@@ -375,7 +378,7 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
     if (e == hipSuccess) e = sched_release(ctx, *lru);
     if (e == hipSuccess) e = hipMalloc(&lru->buf, ((size_t)4 * n + 1024) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 4 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->side);
-    for (hipEvent_t *ev : {&lru->rendered, &lru->sorted[0], &lru->sorted[1]})
+    for (hipEvent_t *ev : {&lru->rendered, &lru->sorted[0], &lru->sorted[1], &lru->last})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         (void)sched_release(ctx, *lru);
@@ -421,16 +424,17 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         }
     }
     if (ctx->scene != rm::SCENE_PLUGIN && pick_kernel(ctx) == rm::KERNEL_PERSIST) {
-        // counters zeroed once; each launch leaves its pair zeroed.  Launches
-        // of one ctx on different streams use different pairs while fewer than
-        // kPersistSlots are in flight.
-        if (!ctx->persist) {
-            const size_t bytes = (size_t)rm::kPersistWords * kPersistSlots * sizeof(uint32_t);
-            RM_HIP(hipMalloc(&ctx->persist, bytes));
-            RM_HIP(hipMemsetAsync(ctx->persist, 0, bytes, ctx->stream));
-            RM_HIP(hipStreamSynchronize(ctx->stream));  // zero before any stream's first launch
+        // this stream's counters, zeroed once; each launch leaves them zeroed
+        for (auto &sp : ctx->persist)
+            if (sp.first == ctx->stream) F.persist = sp.second;
+        if (!F.persist) {
+            const size_t bytes = (size_t)rm::kPersistWords * sizeof(uint32_t);
+            uint32_t *blk = nullptr;
+            RM_HIP(hipMalloc(&blk, bytes));
+            ctx->persist.emplace_back(ctx->stream, blk);
+            RM_HIP(hipMemsetAsync(blk, 0, bytes, ctx->stream));
+            F.persist = blk;
         }
-        F.persist = ctx->persist + (size_t)rm::kPersistWords * (ctx->persist_k++ % kPersistSlots);
     }
     bool cnt = ctx->params.count_evals != 0 || evmap;
     if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 2 * sizeof(unsigned long long), ctx->stream));
@@ -451,7 +455,10 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
         RM_HIP(hipEventRecord(sc->sorted[slot], ctx->side));
     }
-    if (sc) sc->k++;
+    if (sc) {
+        RM_HIP(hipEventRecord(sc->last, ctx->stream));
+        sc->k++;
+    }
     if (stats) {
         RM_HIP(hipEventSynchronize(ctx->ev1));
         float ms = 0.0f;
@@ -586,10 +593,12 @@ rm_status rm_create(rm_ctx **out, int device) {
 rm_status rm_destroy(rm_ctx *ctx) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);  // nothing of this context still runs
+    // nothing of this context still runs (its stream may be the caller's and
+    // already destroyed, so the device is synchronized instead)
+    (void)hipDeviceSynchronize();
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
-    if (ctx->persist) (void)hipFree(ctx->persist);
+    for (auto &sp : ctx->persist) (void)hipFree(sp.second);
     if (ctx->staging) (void)hipFree(ctx->staging);
     if (ctx->mips) (void)hipFree(ctx->mips);
     if (ctx->tile_order) (void)hipFree(ctx->tile_order);

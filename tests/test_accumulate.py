@@ -150,19 +150,21 @@ def test_host_accumulator_equals_device(R, torch_cuda):
 
 
 @pytest.mark.gpu
-def test_headless_host_accumulates(tmp_path, torch_cuda):
+@pytest.mark.parametrize("fmt", ["rgba8", "float"])
+def test_headless_host_accumulates(tmp_path, torch_cuda, fmt):
     """apps/raymarch_headless --accumulate: main.cpp's loop driving the
     plumbing (u_sample_part = 1/framesStill, fresh u_seed1 per frame) through
     rm::RenderTexture::drawAccumulate.  Six still frames average six sub-pixel
     offsets: away from edges the mean is the pixel-centre frame of the oracle,
-    on edges it is antialiased (differs)."""
+    on edges it is antialiased (differs).  In the RGBA8 target (the reference's
+    ping-pong textures) and in RGBA32F."""
     import json
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.dirname(__file__)), "apps", "raymarch_headless")
     ppm = tmp_path / "acc.ppm"
     out = subprocess.run([exe, "--scene", "template.frag", "--w", "96", "--h", "54", "--frames", "6", "--script",
-                          "W", "--time-freeze", "--accumulate", "--ppm", str(ppm)], capture_output=True, text=True,
+                          "W", "--time-freeze", "--accumulate", "--format", fmt, "--ppm", str(ppm)], capture_output=True, text=True,
                          timeout=120)
     assert out.returncode == 0, out.stderr
     info = json.loads(out.stdout.strip().splitlines()[-1])

@@ -483,6 +483,27 @@ def test_headless_cpp_host_app_sharded_path(tmp_path, torch_cuda):
     assert imgs[0] == imgs[1]
 
 
+def test_headless_cpp_host_app_formats_and_stats(tmp_path, torch_cuda):
+    """rm::RenderTexture's RGBA8 target (rm_render_rgba8, the default) and its
+    RGBA32F target packed on copy give the same bytes; --stats adds the per-frame
+    kernel time, without it the frames are queued with no per-frame sync."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(__file__)), "apps", "raymarch_headless")
+    imgs, infos = [], []
+    for extra in (["--format", "rgba8"], ["--format", "float", "--stats"], ["--warmup", "2"]):
+        ppm = tmp_path / f"f{len(imgs)}.ppm"
+        out = subprocess.run([exe, "--scene", "output_shader.frag", "--w", "100", "--h", "60", "--frames", "4",
+                              "--script", "WD..", "--time-freeze", "--ppm", str(ppm)] + extra,
+                             capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        infos.append(json.loads(out.stdout.strip().splitlines()[-1]))
+        imgs.append(ppm.read_bytes())
+    assert imgs[0] == imgs[1]
+    assert infos[0]["format"] == "rgba8" and infos[1]["format"] == "float"
+    assert "kernel_ms_per_frame" not in infos[0] and infos[1]["kernel_ms_per_frame"] > 0
+    assert infos[2]["warmup"] == 2 and infos[2]["frames"] == 4 and infos[2]["fps_wall"] > 0
+
+
 def test_render_rows_chunks_and_frame_pipeline(R, torch_cuda):
     """rm_render_rows sub-ranges reassemble the band exactly; the chunked
     single-rank DistributedFrame equals rm_render_rgba8."""

@@ -8,6 +8,10 @@ Per launch of the render kernel:
       MI355X_MICROARCH.md "HBM"; WRITE_SIZE is exact for the RGBA8 stores,
       checked against the 64 MiB frame)
   flop_exec = 64 * (ADD + MUL + TRANS + 2 * FMA) executed F32 wave-instructions
+      (issued lane slots: 64 per wave-instruction whatever the exec mask)
+  active_lane_frac = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU): the
+      mean fraction of a VALU instruction's lanes that are active (exec mask)
+  flop_lanes = flop_exec * active_lane_frac: FP32 FLOP done by active lanes
   clock_hz = GRBM_GUI_ACTIVE / 8 XCDs / the kernel's average duration (from
       the kernel-trace stats of the same command)
 usage: make_traffic_json.py SUMMARY.json KEY KERNEL_SUBSTR KERNEL_STATS.csv [OUT]
@@ -28,7 +32,7 @@ entry = {"kernel": k, "source": os.path.relpath(summ), "kernel_stats": os.path.r
 if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
     entry.update(FETCH_SIZE_KiB=v["FETCH_SIZE"], WRITE_SIZE_KiB=v["WRITE_SIZE"],
                  hbm_bytes_per_launch=(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024)
-for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE", "SQ_INSTS_BRANCH",
+for c in ("SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE", "SQ_INSTS_BRANCH",
           "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32",
           "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES"):
     if c in v:
@@ -36,6 +40,10 @@ for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "
 f32 = ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32")
 if all(c in v for c in f32):
     entry["flop_exec_per_launch"] = 64 * (v[f32[0]] + v[f32[1]] + v[f32[2]] + 2 * v[f32[3]])
+if "SQ_THREAD_CYCLES_VALU" in v and "SQ_ACTIVE_INST_VALU" in v:
+    entry["active_lane_frac"] = v["SQ_THREAD_CYCLES_VALU"] / (64 * v["SQ_ACTIVE_INST_VALU"])
+    if "flop_exec_per_launch" in entry:
+        entry["flop_lanes_per_launch"] = entry["flop_exec_per_launch"] * entry["active_lane_frac"]
 if "GRBM_GUI_ACTIVE" in v:
     entry["clock_hz"] = v["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9)
 allj = json.load(open(out)) if os.path.exists(out) else {}
