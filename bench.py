@@ -314,20 +314,22 @@ def main():
     # instrumented run: ray-steps of this rank's rows, summed over ranks (with
     # --walk: per timed pose, their mean is the frame's count)
     r.set_params(count_evals=1)
-    walk_evals = []
+    walk_evals, walk_skipped = [], []
     for i in range(args.steps if args.walk else 1):
         set_frame(i)
         _, st = fr.render_local(stats=True)
         walk_evals.append(st["evals"])
+        walk_skipped.append(st.get("skipped", 0))
     if args.walk:
-        st = dict(st, evals=sum(walk_evals) / len(walk_evals))
+        st = dict(st, evals=sum(walk_evals) / len(walk_evals), skipped=sum(walk_skipped) / len(walk_skipped))
     r.set_params(count_evals=0)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
-    ev_rank = torch.tensor([st["evals"]], dtype=torch.float64, device=red_dev)
+    ev_rank = torch.tensor([st["evals"], st.get("skipped", 0)], dtype=torch.float64, device=red_dev)
     ev_total = ev_rank.clone()
     if world > 1:
         dist.all_reduce(ev_total)
-    evals_rank, evals_frame = int(ev_rank.item()), int(ev_total.item())
+    evals_rank, evals_frame = int(ev_rank[0].item()), int(ev_total[0].item())
+    skipped_frame = int(ev_total[1].item())
 
     # untimed spin-up before the W warm-up frames: a fresh GPU ramps its clocks
     # over the first ~0.1 s of load (3 warm-up frames are ~3 ms), so the timed
@@ -422,11 +424,17 @@ def main():
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
                 "band": args.band, "fmt": args.fmt, "wire": fr.wire, "streams": len(fr.streams), "kernel": args.kernel, "chunks": chunks, "schedule": args.schedule,
                 "ray_steps_per_frame": evals_frame, "ray_steps_per_px": evals_frame / (W * H),
+                "executed_ray_steps_per_frame": evals_frame - skipped_frame,
                 "walk": None if not args.walk else {
                     "speed": args.walk_speed, "dt": args.walk_dt, "frames": args.steps,
                     "rank0_ray_steps_min": min(walk_evals), "rank0_ray_steps_max": max(walk_evals),
                     "end_pose": walk_pose(pose, args.steps - 1, args.walk_speed, args.walk_dt)},
             },
+            "value_note": "value counts the reference's ray-steps (sceneSDF calls of common.frag's loops) per "
+                          "frame; the kernels leave out steps that provably cannot change the frame (exact early "
+                          "exits: settled soft shadows, DESIGN.md 2.11), so they execute "
+                          "executed_ray_steps_per_s; frames_per_s is the same either way",
+            "executed_ray_steps_per_s": (evals_frame - skipped_frame) * args.steps / elapsed,
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max, "frame_stream_ms": frame_stream_ms,
             "kernel_ms_note": "median per-launch duration of the render kernel (HIP events on its stream, "
                               "synchronous launches after the timed region, adaptive dispatch order as in the "

@@ -66,6 +66,10 @@ typedef struct rm_stats {
     uint64_t flop;   /* algorithmic FLOP of those calls, when count_evals: the per-term
                         tally of SURVEY.md 8(d) over the terms evaluated (exact early
                         exits skip Menger folds and scene O's primitives)          */
+    uint64_t skipped; /* when count_evals: of `evals`, the ray-steps the uninstrumented
+                        kernels do not execute (exact early exits whose results equal
+                        the reference's: scene T's settled soft shadows, DESIGN.md
+                        2.11); executed = evals - skipped                            */
 } rm_stats;
 
 /* Create a context on HIP device `device`.  Scene unset, params default. */

@@ -90,6 +90,9 @@ def lib(fast: bool = False) -> ctypes.CDLL:
         L.oracle_render_diag.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, f32p, f32p]
         L.oracle_render_diag.restype = ctypes.c_int
+        L.oracle_shadow_settle.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p]
+        L.oracle_shadow_settle.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         L.oracle_num_threads.restype = ctypes.c_int
         _LIBS[name] = L
@@ -183,6 +186,18 @@ def render_pixels(scene: str, W: int, H: int, xs, ys, fast=False, **kw):
     if rc:
         raise ValueError(f"oracle_render_pixels failed rc={rc}")
     return out, ev
+
+
+def shadow_settle(scene: str, W: int, H: int, **kw):
+    """Analysis aid: the soft-shadow settle rule applied to
+    every step of the reference's shadow marches of a W x H frame ->
+    dict(marches, steps, after, settled, violations); `violations` counts
+    changes of res (or occlusions) after a march settled."""
+    u = uniforms(W, H, **kw)
+    out = np.zeros(5, np.uint64)
+    if lib().oracle_shadow_settle(SCENES[scene], ctypes.byref(u), W, H, 0, H, out.ctypes.data):
+        raise ValueError("oracle_shadow_settle failed")
+    return dict(zip(("marches", "steps", "after", "settled", "violations"), (int(v) for v in out)))
 
 
 N_DIAG = 7

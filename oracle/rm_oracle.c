@@ -77,6 +77,7 @@ typedef struct {
     struct SegRec *rec; /* optional: per-pixel phase/segment recorder (analysis) */
     float *diag;        /* optional: scene-O diagnostic channels, N_DIAG vec4 per pixel */
     int lvl;            /* 0 = primary light(), 1 = inside the reflection bounce */
+    struct SettleRec *settle; /* optional: soft-shadow settle analysis (scenes T, O) */
 } Ctx;
 
 /* Diagnostic channels of make_goldens.py diag_edit (test aid, values only):
@@ -390,19 +391,88 @@ static vec3 phongContribForLight(vec3 k_d, vec3 k_s, float alpha, vec3 p, vec3 e
 }
 
 /* common.frag:810-831.  max_steps == 0: unbounded, as the reference. */
+/* Analysis aid (not part of the restatement): the soft-shadow "settle" test
+ * of DESIGN.md 2.11 evaluated at every step of scene T's shadow marches: the
+ * step at which it first holds, the steps after it, and any change of res (or
+ * an occlusion) after it -- which the test's proof says cannot happen. */
+typedef struct SettleRec {
+    uint64_t marches, steps, after, settled, violations;
+} SettleRec;
+static int settle_test(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, float res) {
+    /* sponge space: q(t) = transformR(p - (0,3,0)), dq/dt = transformR(rd) (linear) */
+    vec3 q = transformR(C, sub(p, v3(0.0f, 3.0f, 0.0f))), d = transformR(C, rd);
+    float ax = fabsf(q.x), ay = fabsf(q.y), az = fabsf(q.z);
+    float m = fmaxf(ax, fmaxf(ay, az)), B = m - 1.0f;
+    float sl = ax == m ? (q.x < 0 ? -d.x : d.x) : ay == m ? (q.y < 0 ? -d.y : d.y) : (q.z < 0 ? -d.z : d.z);
+    if (!(B >= 0.1f) || !(sl >= 0.0f)) return 0;
+    float be = B + sl * (maxt - t);
+    float lo = fminf(B / t, be / maxt);
+    return 2.9f * lo >= 1.01f * res;
+}
+
+/* The same rule for scene O: sceneSDF >= min(sponge box,
+ * sphere, Chebyshev bound of the cube, plane) - (0.5 + 0.5 + 0.33) / 6 (each
+ * sminCubic lowers a min by at most k/6); each term is convex along the ray
+ * (the plane linear), so each has an affine minorant through its value and a
+ * subgradient at t, and the bound's ratio to t' is smallest at t or maxt. */
+static int settle_piece(float v, float sl, float t, float maxt, float res, float *lo) {
+    const float off = (0.5f + 0.5f + 0.33f) / 6.0f;
+    float g0 = v - off, g1 = v + sl * (maxt - t) - off;
+    if (!(g0 >= 0.1f) || !(g1 >= 0.1f)) return 0;
+    float r = fminf(g0 / t, g1 / maxt);
+    *lo = fminf(*lo, r);
+    (void)res;
+    return 1;
+}
+static int settle_test_O(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, float res) {
+    vec3 q = transformR(C, sub(p, v3(0.0f, 3.0f, 0.0f))), d = transformR(C, rd);
+    float ax = fabsf(q.x), ay = fabsf(q.y), az = fabsf(q.z);
+    float m = fmaxf(ax, fmaxf(ay, az));
+    float s0 = ax == m ? (q.x < 0 ? -d.x : d.x) : ay == m ? (q.y < 0 ? -d.y : d.y) : (q.z < 0 ? -d.z : d.z);
+    vec3 e1 = sub(p, v3(3.0f, 2.0f, 3.0f));
+    float l1 = length3(e1);
+    vec3 e2 = sub(p, v3(-5.0f, 4.0f, 5.0f));
+    float bx = fabsf(e2.x), by = fabsf(e2.y), bz = fabsf(e2.z), m2 = fmaxf(bx, fmaxf(by, bz));
+    float s2 = bx == m2 ? (e2.x < 0 ? -rd.x : rd.x) : by == m2 ? (e2.y < 0 ? -rd.y : rd.y) : (e2.z < 0 ? -rd.z : rd.z);
+    float lo = 1e30f;
+    if (!settle_piece(m - 1.0f, s0, t, maxt, res, &lo)) return 0;
+    if (!settle_piece(l1 - 1.0f, dot3(e1, rd) / l1, t, maxt, res, &lo)) return 0;
+    if (!settle_piece(m2 - 1.0f, s2, t, maxt, res, &lo)) return 0;
+    if (!settle_piece(p.y, rd.y, t, maxt, res, &lo)) return 0;
+    return 2.9f * lo >= 1.01f * res;
+}
+
 static float softshadow2(const Ctx *C, vec3 ro, vec3 rd, float mint, float maxt, float k) {
     seg_begin(C, PH_SHADOW);
     float res = 1.0f;
     float ph = 1e20f;
     int it = 0;
+    SettleRec *S = C->settle;
+    int settled = 0;
+    float res_at = 0.0f;
+    if (S) S->marches++;
     for (float t = mint; t < maxt;) {
         if (C->u.shadow_max_steps > 0 && it++ >= C->u.shadow_max_steps) break;
         float h = sceneSDF(C, add(ro, muls(rd, t))).dist;
-        if (h < 0.001f) return 0.0f;
+        if (S) {
+            S->steps++;
+            if (settled) S->after++;
+        }
+        if (h < 0.001f) {
+            if (S && settled) S->violations++;
+            return 0.0f;
+        }
         float y = h * h / (2.0f * ph);
         float d = sqrtf(h * h - y * y);
         res = gmin(res, k * d / gmax(0.0f, t - y));
         ph = h;
+        if (S) {
+            if (settled && res != res_at) S->violations++, res_at = res;
+            vec3 pt = add(ro, muls(rd, t));
+            if (!settled && (C->scene == SCENE_T ? settle_test(C, pt, rd, t, maxt, res)
+                                                 : settle_test_O(C, pt, rd, t, maxt, res)))
+                settled = 1, res_at = res, S->settled++;
+        }
         t += h * 0.1f + 0.001f;
     }
     return res;
@@ -836,6 +906,31 @@ int oracle_render_pixels(int scene, const oracle_uniforms *u, int W, int H, cons
         shade_pixel(&C, W, H, xy[2 * i], xy[2 * i + 1], out + (size_t)i * 4);
         if (evals) evals[i] = (uint32_t)cnt;
     }
+    return 0;
+}
+
+/* Soft-shadow settle analysis (analysis aid) over rows [row0, row0+nrows):
+ * out[5] = marches, steps, steps after the settle point, settled marches,
+ * violations (res changed or occluded after settling). */
+int oracle_shadow_settle(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, uint64_t *out) {
+    if (!u || !out || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H) return 1;
+    uint64_t acc[5] = {0, 0, 0, 0, 0};
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; r++) {
+        Ctx C;
+        uint64_t cnt = 0;
+        SettleRec S = {0, 0, 0, 0, 0};
+        float px[4];
+        init_ctx(&C, scene, u);
+        C.evals = &cnt;
+        C.settle = &S;
+        for (int x = 0; x < W; x++) shade_pixel(&C, W, H, x, row0 + r, px);
+#pragma omp critical
+        {
+            acc[0] += S.marches; acc[1] += S.steps; acc[2] += S.after; acc[3] += S.settled; acc[4] += S.violations;
+        }
+    }
+    for (int i = 0; i < 5; i++) out[i] = acc[i];
     return 0;
 }
 

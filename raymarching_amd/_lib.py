@@ -35,11 +35,11 @@ class RmParams(ctypes.Structure):
 
 class RmStats(ctypes.Structure):
     _fields_ = [("evals", ctypes.c_uint64), ("pixels", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
-                ("scene", ctypes.c_int32), ("flop", ctypes.c_uint64)]
+                ("scene", ctypes.c_int32), ("flop", ctypes.c_uint64), ("skipped", ctypes.c_uint64)]
 
     def as_dict(self):
         return dict(evals=int(self.evals), pixels=int(self.pixels), kernel_ms=float(self.kernel_ms),
-                    scene=int(self.scene), flop=int(self.flop))
+                    scene=int(self.scene), flop=int(self.flop), skipped=int(self.skipped))
 
 
 class RmShardLayout(ctypes.Structure):

@@ -68,7 +68,7 @@ struct rm_ctx {
     struct Sched {
         uint64_t key = 0;
         hipStream_t stream = nullptr;
-        int n = 0;
+        int n = 0, gx = 0;         // tiles, tile-grid width
         uint64_t k = 0;            // launches so far
         uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256])
         hipEvent_t rendered = nullptr, sorted[2] = {nullptr, nullptr};
@@ -275,6 +275,16 @@ int sched_period() {
     return n;
 }
 
+// Dilation radius (tiles) of the sort key (rm_kernels.hip tile_key):
+// RM_SCHED_DILATE, default 0.
+int sched_dilate() {
+    static const int n = [] {
+        const char *e = std::getenv("RM_SCHED_DILATE");
+        return e ? std::max(0, std::min(8, std::atoi(e))) : 0;
+    }();
+    return n;
+}
+
 FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int shard, int nrows) {
     FrameConst F;
     std::memset(&F, 0, sizeof(F));
@@ -388,6 +398,7 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
     lru->key = key;
     lru->stream = ctx->stream;
     lru->n = n;
+    lru->gx = g.x;
     lru->used = ++ctx->sched_clock;
     return lru;
 }
@@ -437,7 +448,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         }
     }
     bool cnt = ctx->params.count_evals != 0 || evmap;
-    if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 3 * sizeof(unsigned long long), ctx->stream));
     if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     hipError_t e =
         ctx->scene == rm::SCENE_PLUGIN
@@ -450,7 +461,8 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         uint32_t *h = sc->buf + 4 * (size_t)sc->n;
         RM_HIP(hipEventRecord(sc->rendered, ctx->stream));
         RM_HIP(hipStreamWaitEvent(ctx->side, sc->rendered, 0));
-        e = rm::launch_tile_order(sc->buf + slot * sc->n, sc->n, sc->buf + (2 + slot) * sc->n, h + 512 * slot,
+        e = rm::launch_tile_order(sc->buf + slot * sc->n, sc->n, sc->gx, sched_dilate(), sc->buf + (2 + slot) * sc->n,
+                                  h + 512 * slot,
                                   h + 512 * (1 - slot), ctx->side);
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
         RM_HIP(hipEventRecord(sc->sorted[slot], ctx->side));
@@ -463,10 +475,11 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         RM_HIP(hipEventSynchronize(ctx->ev1));
         float ms = 0.0f;
         RM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-        unsigned long long ev[2] = {0, 0};
+        unsigned long long ev[3] = {0, 0, 0};
         if (cnt) RM_HIP(hipMemcpy(ev, ctx->d_evals, sizeof(ev), hipMemcpyDeviceToHost));
         stats->evals = ev[0];
         stats->flop = ev[1];
+        stats->skipped = ev[2];
         stats->pixels = (uint64_t)W * (uint64_t)count;
         stats->kernel_ms = ms;
         stats->scene = ctx->scene;
@@ -489,7 +502,7 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     if (row_begin < 0 || row_count < 0 || row_begin + row_count > n)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: packed row range outside the shard");
     if (row_count == 0) {  // e.g. more shards than bands: nothing to do
-        if (stats) *stats = rm_stats{0, 0, 0.0f, ctx->scene, 0};
+        if (stats) *stats = rm_stats{0, 0, 0.0f, ctx->scene, 0, 0};
         return RM_OK;
     }
     if (!out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: null output");
@@ -579,7 +592,7 @@ rm_status rm_create(rm_ctx **out, int device) {
     rm_ctx *ctx = new rm_ctx();
     ctx->device = device;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_evals, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_evals, 3 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
     if (e != hipSuccess) {

@@ -156,6 +156,7 @@ __host__ __device__ inline float glsl_cos(float x) { return glsl_sin(x + 1.57079
 struct Tally {
     uint32_t evals = 0;
     uint32_t flop = 0;
+    uint32_t skipped = 0;  // of evals: steps the timed kernels leave out (exact early exits)
 };
 constexpr uint32_t FL_SPHERE = 9;      // sphere(): sub 3, dot 5, sub 1 (+ sqrt)
 constexpr uint32_t FL_TRANSFORM = 18;  // p - (0,3,0): 3; transformR's 3x3 rotation: 15

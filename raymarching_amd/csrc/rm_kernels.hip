@@ -102,18 +102,34 @@ __global__ __launch_bounds__(256) void rm_deinterleave_rgb8(const uint8_t* __res
 // the tile's rank in the block, and clears the other parity's histogram and
 // cursors (`next`) for the following sort (no memset on the stream).  The
 // context runs both on a side stream, overlapping the next frame's render.
-__global__ __launch_bounds__(256) void rm_sched_hist(const uint32_t* __restrict__ cost, int n,
+// The sort key of tile i: its duration, or with a dilation radius r > 0 the
+// longest duration among the tiles within r of it on the gx-wide tile grid
+// (an order that stays right while the costly regions move a few tiles
+// between the launch that measured them and the launches that use the order).
+__device__ __forceinline__ uint32_t tile_key(const uint32_t* __restrict__ cost, int i, int n, int gx, int r) {
+    if (r <= 0) return cost[i];
+    const int x = i % gx, y = i / gx;
+    uint32_t m = 0;
+    for (int yy = max(0, y - r); yy <= y + r; yy++)
+        for (int xx = max(0, x - r); xx <= min(gx - 1, x + r); xx++) {
+            const int j = yy * gx + xx;
+            if (j < n) m = max(m, cost[j]);
+        }
+    return m;
+}
+
+__global__ __launch_bounds__(256) void rm_sched_hist(const uint32_t* __restrict__ cost, int n, int gx, int r,
                                                       uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[kSchedBuckets];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int end = min(n, (int)(blockIdx.x + 1) * 1024);
-    for (int i = blockIdx.x * 1024 + threadIdx.x; i < end; i += 256) atomicAdd(&h[sched_bucket(cost[i])], 1u);
+    for (int i = blockIdx.x * 1024 + threadIdx.x; i < end; i += 256) atomicAdd(&h[sched_bucket(tile_key(cost, i, n, gx, r))], 1u);
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restrict__ cost, int n,
+__global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restrict__ cost, int n, int gx, int r,
                                                          const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor,
                                                          uint32_t* __restrict__ order, uint32_t* __restrict__ next) {
     __shared__ uint32_t base[kSchedBuckets], cnt[kSchedBuckets];
@@ -137,7 +153,7 @@ __global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restri
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int i = i0 + 256 * k;
-        b[k] = i < n ? sched_bucket(cost[i]) : -1;
+        b[k] = i < n ? sched_bucket(tile_key(cost, i, n, gx, r)) : -1;
         rank[k] = b[k] >= 0 ? atomicAdd(&cnt[b[k]], 1u) : 0;
     }
     __syncthreads();
@@ -148,13 +164,13 @@ __global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restri
         if (b[k] >= 0) order[base[b[k]] + rank[k]] = (uint32_t)(i0 + 256 * k);
 }
 
-hipError_t launch_tile_order(const uint32_t* cost, int n, uint32_t* order, uint32_t* hist, uint32_t* next,
-                             hipStream_t s) {
-    if (n <= 0) return hipSuccess;
+hipError_t launch_tile_order(const uint32_t* cost, int n, int gx, int radius, uint32_t* order, uint32_t* hist,
+                             uint32_t* next, hipStream_t s) {
+    if (n <= 0 || gx <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n + 1023) / 1024);
-    hipLaunchKernelGGL(rm_sched_hist, dim3(blocks), dim3(256), 0, s, cost, n, hist);
-    hipLaunchKernelGGL(rm_sched_scatter, dim3(blocks), dim3(256), 0, s, cost, n, hist, hist + kSchedBuckets, order,
-                       next);
+    hipLaunchKernelGGL(rm_sched_hist, dim3(blocks), dim3(256), 0, s, cost, n, gx, radius, hist);
+    hipLaunchKernelGGL(rm_sched_scatter, dim3(blocks), dim3(256), 0, s, cost, n, gx, radius, hist,
+                       hist + kSchedBuckets, order, next);
     return hipGetLastError();
 }
 

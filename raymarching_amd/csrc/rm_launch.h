@@ -36,8 +36,8 @@ hipError_t launch_deinterleave_rgb8(const uint8_t* gathered, uint32_t* out, int 
 // the next launch's tile order (costliest first) from the tile durations
 // (hist: 256 counts + 256 cursors, zero on entry); clears `next` (512 words)
 // for the following launch
-hipError_t launch_tile_order(const uint32_t* cost, int n, uint32_t* order, uint32_t* hist, uint32_t* next,
-                             hipStream_t s);
+hipError_t launch_tile_order(const uint32_t* cost, int n, int gx, int radius, uint32_t* order, uint32_t* hist,
+                             uint32_t* next, hipStream_t s);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 
 // bloom.frag's textureLod level pair and the mip levels 1..d2 it needs,

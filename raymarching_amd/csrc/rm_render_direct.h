@@ -212,15 +212,43 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // vanish: the candidate is k h / t (Q = 1, D = t below).  The occlusion result
 // is recovered after the loop from the last h (a lane leaves through
 // t >= maxt only with h >= 0.001).
-template <bool CAP, int NB>
+//
+// SETTLE (the timed kernels): a lane leaves the march as soon
+// as no later step can change its result.  Every later step t' has h' >= B(t')
+// (the sponge's box term, a lower bound of mengersponge), and B along the
+// sponge-space ray, max_i |o_i + d_i t'| - 1, is convex: B(t') >= g(t') =
+// B(t) + s (t' - t) with s = d_i sign(q_i) on an axis attaining the max.  If
+// B(t) >= 0.1 and s >= 0, every later h' >= 0.1 (no occlusion) and the
+// previous h >= 0.1, so with mengersponge 3-Lipschitz and the step 0.1 ph +
+// 0.001, h' / (2 ph) <= 0.665 and every later candidate
+// k h' sqrt(1 - (h'/2ph)^2) / (t' - y) is >= 4 * 0.7469 g(t') / t'.  g / t'
+// is monotonic, so its minimum over [t, maxt] is at an endpoint: when
+// 2.9 min(B / t, g(maxt) / maxt) >= 1.01 res no later candidate lowers res
+// (margins far above the roundings), and the result is res now.  The test
+// runs when some lane of the wave has B >= 0.1 and h >= ph (a march moving
+// away from the sponge).  tools: oracle_shadow_settle checks the rule on every
+// step of the reference's marches (no change of res after it, ever) and
+// measures 43-55 % of scene T's shadow steps after it.  The instrumented
+// kernels (COUNT) keep every step: their ray-step counts and maps are the
+// reference's.
+// SM: 0 no settle test, 1 leave the march when settled (timed kernels), 2 run
+// the test and count the steps after it in cnt.skipped (instrumented kernels:
+// every reference step is still taken and counted)
+template <bool CAP, int NB, int SM = 0>
 __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                      Tally& cnt) {
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
     float t = mint;
-    // one exit test per step (occluded, t >= maxt, or the optional step cap);
-    // t grows by >= 0.001 per continuing step, NaN leaves
+    bool was_settled = false;  // SM == 2
+    // one exit test per step (occluded, t >= maxt, settled, or the optional
+    // step cap); t grows by >= 0.001 per continuing step, NaN leaves
     for (int it = 1; it == 1 ? t < maxt : true; it++) {
-        h = menger_at<NB>(s, t, cnt);
+        const V3 q = at(s, t);
+        const float box = sponge_box(q);
+        cnt.evals++;
+        cnt.flop += FL_LINRAY + FL_BOX;
+        if constexpr (SM == 2) cnt.skipped += was_settled ? 1u : 0u;
+        h = sponge_folds<false, NB>(q, box, cnt.flop);
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
         float D = it == 1 ? t : fmaf(t, P, -h2);
@@ -228,12 +256,29 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
         bool upd = (Q >= 0.0f) & (cn * den < num * cd);
         num = upd ? cn : num;
         den = upd ? cd : den;
+        bool settled = false;
+        if constexpr (SM != 0) {
+            if (__builtin_amdgcn_ballot_w64((box >= 0.1f) & (h + h >= P)) != 0) {
+                const float ax = fabsf(q.x), ay = fabsf(q.y), m = box + 1.0f;
+                const float sx = q.x < 0.0f ? -s.d.x : s.d.x, sy = q.y < 0.0f ? -s.d.y : s.d.y;
+                const float sz = q.z < 0.0f ? -s.d.z : s.d.z;
+                const float sl = ax == m ? sx : ay == m ? sy : sz;
+                const float be = fmaf(sl, maxt - t, box);
+                constexpr float K = (2.9f / 1.01f) * (2.9f / 1.01f) / 16.0f;  // res^2 = 16 num / den
+                settled = (box >= 0.1f) & (h + h >= P) & (sl >= 0.0f) & (K * box * box * den >= num * t * t) &
+                          (K * be * be * den >= num * maxt * maxt);
+            }
+        }
         P = h + h;
 #if RM_SHADOW_P_PIN
         asm volatile("" : "+v"(P));  // keep P's add in the step (not in a continue block of its own)
 #endif
         t = fmaf(h, 0.1f, t + 0.001f);
-        if ((h < 0.001f) | !(t < maxt) | (CAP && it >= F.shadow_max_steps)) break;
+        if constexpr (SM == 2) {
+            was_settled |= settled;
+            settled = false;
+        }
+        if ((h < 0.001f) | !(t < maxt) | settled | (CAP && it >= F.shadow_max_steps)) break;
     }
     return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(16.0f * num * __builtin_amdgcn_rcpf(den));
 }
@@ -245,13 +290,17 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
 // SALU per step, and SALU issue is a co-bottleneck of the kernel.
 // (Scene O's soft_shadow2 measured no gain from the same split: its kernel
 // spills at occupancy 8 and the second loop copy spilled more.)
-template <int NB = 3>
+#ifndef RM_SHADOW_SETTLE
+#define RM_SHADOW_SETTLE 1
+#endif
+template <int NB = 3, int SETTLE = 0>
 __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                 Tally& cnt) {
+    constexpr int ST = RM_SHADOW_SETTLE ? SETTLE : 0;
 #if RM_SHADOW_UNCAPPED_LOOP
-    if (F.shadow_max_steps == __INT_MAX__) return soft_shadow2_T_loop<false, NB>(F, s, mint, maxt, cnt);
+    if (F.shadow_max_steps == __INT_MAX__) return soft_shadow2_T_loop<false, NB, ST>(F, s, mint, maxt, cnt);
 #endif
-    return soft_shadow2_T_loop<true, NB>(F, s, mint, maxt, cnt);
+    return soft_shadow2_T_loop<true, NB, ST>(F, s, mint, maxt, cnt);
 }
 
 // castRay (common.frag:931-954) for scene T in sponge space; returns the
@@ -457,8 +506,8 @@ __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally&
     return color;
 }
 
-// template.frag:45-76 (scene T); NB: sponge_folds
-template <int NB = 3>
+// template.frag:45-76 (scene T); NB: sponge_folds; SETTLE: soft_shadow2_T_loop
+template <int NB = 3, int SETTLE = 0>
 __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     constexpr int SC = SCENE_T;
     V3 p = ro + rd * cast_ray_T<NB>(F, sponge_ray(F, ro, rd), cnt);
@@ -480,7 +529,7 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
 #ifdef RM_ABLATE_SHADOW
     float sha = 1.0f;
 #else
-    float sha = soft_shadow2_T<NB>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
+    float sha = soft_shadow2_T<NB, SETTLE>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
 #endif
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
@@ -575,10 +624,13 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-template <int SC, int NB = 3>
+// SETTLE: the timed kernels' exact early exits (1), which the instrumented
+// (COUNT) kernels do not take but count (2): their ray-step counts and maps
+// stay the reference's, rm_stats.skipped the steps the timed kernels leave out
+template <int SC, int NB = 3, int SETTLE = 0>
 __device__ __forceinline__ V3 render_pixel(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     if constexpr (SC == SCENE_S0) return render_S0(F, ro, rd, cnt);
-    else if constexpr (SC == SCENE_T) return render_T<NB>(F, ro, rd, cnt);
+    else if constexpr (SC == SCENE_T) return render_T<NB, SETTLE>(F, ro, rd, cnt);
     else return render_O<SC>(F, ro, rd, cnt);  // O, OG and plugins: output_shader.frag's render()
 }
 
@@ -619,7 +671,7 @@ template <> struct Tiling<KERNEL_PERSIST> : Tiling<KERNEL_TILE8> {};
 // OUT = float4 (gl_FragColor) or uint32_t (RGBA8, packed in the epilogue, so
 // the displayed frame costs 4 B/px of HBM instead of 16 + 20 for a pack
 // pass).  COUNT: instrumented build, ray-steps and FLOP summed per wave into
-// evals[0..1].
+// evals[0..2] (ray-steps, FLOP, ray-steps the timed kernels skip).
 // (bx, by): the tile's position in dispatch order on a gx-wide tile grid
 // (blockIdx for the hardware-dispatched kernels).
 template <int SC, bool COUNT, int K, typename OUT>
@@ -649,8 +701,11 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
         const float vig = vignette<FastMath<SC>::value>(tcx, tcy);
         V3 c;
         if constexpr (SC == SCENE_T) {
-            if (lat) c = render_pixel<SC, 1>(F, ro, rd, cnt);
-            else c = render_pixel<SC>(F, ro, rd, cnt);
+            // (no settle exit in the latency tiles: their long grazing shadow marches
+            // settle late or never, and the test lengthens the lone waves that end
+            // the launch: C4 share +16 %, C2 P1 +12 % with it)
+            if (lat) c = render_pixel<SC, 1, 0>(F, ro, rd, cnt);
+            else c = render_pixel<SC, 3, COUNT ? 2 : 1>(F, ro, rd, cnt);
         } else {
             (void)lat;
             c = render_pixel<SC>(F, ro, rd, cnt);
@@ -664,10 +719,11 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
     }
     if constexpr (COUNT) {
         if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;
-        uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop);
+        uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop), ss = wave_sum_u32(cnt.skipped);
         if (lane == 0) {
             atomicAdd(&evals[0], (unsigned long long)se);
             atomicAdd(&evals[1], (unsigned long long)sf);
+            if (ss) atomicAdd(&evals[2], (unsigned long long)ss);
         }
     }
 }

@@ -777,3 +777,29 @@ def test_persistent_waves_equal_hardware_dispatch(R, torch_cuda, scene):
         assert torch.equal(a, ref), i
         assert torch.equal(b, band), i
     R.set_params(kernel="auto")
+
+
+@pytest.mark.parametrize("pose", list(POSES))
+def test_settled_soft_shadows_keep_pixels(R, torch_cuda, pose):
+    """Scene T's timed kernels leave a soft-shadow march once no later step can
+    change it; the instrumented kernel takes every reference
+    step and counts the ones left out (rm_stats.skipped).  The timed frame
+    (row-major and ordered, float4 and RGBA8) equals the instrumented frame bit
+    for bit, the step map stays the reference's, and the share of steps left
+    out is the oracle's share of steps after the settle point, within 2 %."""
+    torch = torch_cuda
+    setup(R, "T", POSES[pose], 128)
+    W, H = 192, 108
+    R.set_params(schedule=0)
+    ref, st = R.render(W, H, stats=True)
+    assert st["skipped"] > 0
+    R.set_params(count_evals=0)
+    assert torch.equal(R.render(W, H), ref)
+    R.set_params(schedule=1)
+    ref8 = R.pack_rgba8(ref)
+    for _ in range(3):
+        assert torch.equal(R.render_rgba8(W, H), ref8)
+    p = POSES[pose]
+    o = oracle.shadow_settle("T", W, H, pos=p["pos"], mouse=p["mouse"], time=p["time"], max_steps=128)
+    frac_hip, frac_ref = st["skipped"] / st["evals"], o["after"] / st["evals"]
+    assert abs(frac_hip - frac_ref) <= 0.02, (frac_hip, frac_ref, st, o)

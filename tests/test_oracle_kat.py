@@ -159,3 +159,20 @@ def test_render_pixels_equals_rows():
     assert np.array_equal(ev.ravel(), ev2)
     with pytest.raises(ValueError):
         oracle.render_pixels("O", 320, 200, [320], [0])
+
+
+@pytest.mark.parametrize("scene,steps", [("T", 256), ("O", 512)])
+def test_shadow_settle_rule_never_changes_a_result(scene, steps):
+    """once the settle rule holds on a soft-shadow march, no
+    later step of the reference's march lowers res or occludes -- checked on
+    every step of every march of frames at all poses (the oracle runs the
+    reference's full loop and tests the rule beside it)."""
+    from raymarching_amd import POSES
+    tot = dict(steps=0, after=0, violations=0)
+    for pose in POSES.values():
+        r = oracle.shadow_settle(scene, 96, 64, pos=pose["pos"], mouse=pose["mouse"], time=pose["time"],
+                                 max_steps=steps)
+        for k in tot:
+            tot[k] += r[k]
+    assert tot["violations"] == 0, tot
+    assert tot["after"] > 0.1 * tot["steps"], tot

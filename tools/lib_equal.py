@@ -3,6 +3,9 @@
 the same frames (float4 image + per-pixel ray-step map) and writes their
 SHA-256; the parent compares them to the first library's.  Used to show that a
 kernel restructuring leaves pixels and step maps unchanged.
+Per frame: the instrumented kernel's image and step map, the timed kernels'
+frames (float4; RGBA8 with the adaptive order), and whether the timed float4
+frame equals the instrumented one.
 Usage: lib_equal.py lib.so [lib.so ...]   (SCENES=O,OG,T, SIZE=512)"""
 import hashlib
 import json
@@ -25,7 +28,15 @@ for scene in os.environ.get("SCENES", "O,OG,T").split(","):
         r.set_params(max_steps=steps, shadow_max_steps=0, count_evals=1, schedule=0)
         img, ev, st = r.render_step_map(size, size * 9 // 16)
         h = hashlib.sha256(img.cpu().numpy().tobytes() + ev.cpu().numpy().tobytes()).hexdigest()
-        out[f"{scene}/{pn}"] = [h, st["evals"]]
+        # the timed (uninstrumented) kernel: float4 and RGBA8, row-major and adaptive order
+        r.set_params(count_evals=0)
+        timed = [r.render(size, size * 9 // 16).cpu().numpy().tobytes()]
+        r.set_params(schedule=1)
+        for _ in range(3):
+            timed.append(r.render_rgba8(size, size * 9 // 16).cpu().numpy().tobytes())
+        ht = hashlib.sha256(b"".join(timed)).hexdigest()
+        same = timed[0] == img.cpu().numpy().tobytes()
+        out[f"{scene}/{pn}"] = [h, st["evals"], ht, same]
 print(json.dumps(out))
 '''
 
