@@ -91,7 +91,7 @@ def lib(fast: bool = False) -> ctypes.CDLL:
                                          ctypes.c_int, f32p, f32p]
         L.oracle_render_diag.restype = ctypes.c_int
         L.oracle_shadow_settle.argtypes = [ctypes.c_int, up, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                           ctypes.c_void_p]
+                                           ctypes.c_int, ctypes.c_void_p]
         L.oracle_shadow_settle.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         L.oracle_num_threads.restype = ctypes.c_int
@@ -188,14 +188,15 @@ def render_pixels(scene: str, W: int, H: int, xs, ys, fast=False, **kw):
     return out, ev
 
 
-def shadow_settle(scene: str, W: int, H: int, **kw):
-    """Analysis aid: the soft-shadow settle rule applied to
-    every step of the reference's shadow marches of a W x H frame ->
+def shadow_settle(scene: str, W: int, H: int, every: int = 1, **kw):
+    """Analysis aid: the soft-shadow settle rule tested on
+    every `every`-th step of the reference's shadow marches of a W x H frame
+    (the kernels test scene O every 8th step, scene T every step) ->
     dict(marches, steps, after, settled, violations); `violations` counts
     changes of res (or occlusions) after a march settled."""
     u = uniforms(W, H, **kw)
     out = np.zeros(5, np.uint64)
-    if lib().oracle_shadow_settle(SCENES[scene], ctypes.byref(u), W, H, 0, H, out.ctypes.data):
+    if lib().oracle_shadow_settle(SCENES[scene], ctypes.byref(u), W, H, 0, H, every, out.ctypes.data):
         raise ValueError("oracle_shadow_settle failed")
     return dict(zip(("marches", "steps", "after", "settled", "violations"), (int(v) for v in out)))
 

@@ -397,6 +397,7 @@ static vec3 phongContribForLight(vec3 k_d, vec3 k_s, float alpha, vec3 p, vec3 e
  * an occlusion) after it -- which the test's proof says cannot happen. */
 typedef struct SettleRec {
     uint64_t marches, steps, after, settled, violations;
+    int every; /* test on steps every, 2 every, ... of a march (1: every step) */
 } SettleRec;
 static int settle_test(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, float res) {
     /* sponge space: q(t) = transformR(p - (0,3,0)), dq/dt = transformR(rd) (linear) */
@@ -410,18 +411,19 @@ static int settle_test(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, float
     return 2.9f * lo >= 1.01f * res;
 }
 
-/* The same rule for scene O: sceneSDF >= min(sponge box,
- * sphere, Chebyshev bound of the cube, plane) - (0.5 + 0.5 + 0.33) / 6 (each
- * sminCubic lowers a min by at most k/6); each term is convex along the ray
- * (the plane linear), so each has an affine minorant through its value and a
- * subgradient at t, and the bound's ratio to t' is smallest at t or maxt. */
-static int settle_piece(float v, float sl, float t, float maxt, float res, float *lo) {
-    const float off = (0.5f + 0.5f + 0.33f) / 6.0f;
+/* The same rule for scene O (rm_render_direct.h
+ * shadow_settled_O): sceneSDF >= min(sponge box - 0.33/6, plane - 0.83/6,
+ * sphere - 1.33/6, Chebyshev bound of the cube - 1.33/6) (each sminCubic
+ * lowers a min by at most k/6; output_shader.frag:38-48 nests sphere and cube
+ * (k 0.5), then the plane (k 0.5), then the sponge (k 0.33)); each term is
+ * convex along the ray (the plane linear), so each has an affine minorant
+ * through its value and a subgradient at t, and the bound's ratio to t' is
+ * smallest at t or maxt. */
+static int settle_piece(float v, float off, float sl, float t, float maxt, float *lo) {
     float g0 = v - off, g1 = v + sl * (maxt - t) - off;
     if (!(g0 >= 0.1f) || !(g1 >= 0.1f)) return 0;
     float r = fminf(g0 / t, g1 / maxt);
     *lo = fminf(*lo, r);
-    (void)res;
     return 1;
 }
 static int settle_test_O(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, float res) {
@@ -435,10 +437,10 @@ static int settle_test_O(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, flo
     float bx = fabsf(e2.x), by = fabsf(e2.y), bz = fabsf(e2.z), m2 = fmaxf(bx, fmaxf(by, bz));
     float s2 = bx == m2 ? (e2.x < 0 ? -rd.x : rd.x) : by == m2 ? (e2.y < 0 ? -rd.y : rd.y) : (e2.z < 0 ? -rd.z : rd.z);
     float lo = 1e30f;
-    if (!settle_piece(m - 1.0f, s0, t, maxt, res, &lo)) return 0;
-    if (!settle_piece(l1 - 1.0f, dot3(e1, rd) / l1, t, maxt, res, &lo)) return 0;
-    if (!settle_piece(m2 - 1.0f, s2, t, maxt, res, &lo)) return 0;
-    if (!settle_piece(p.y, rd.y, t, maxt, res, &lo)) return 0;
+    if (!settle_piece(m - 1.0f, 0.33f / 6.0f, s0, t, maxt, &lo)) return 0;
+    if (!settle_piece(l1 - 1.0f, 1.33f / 6.0f, dot3(e1, rd) / l1, t, maxt, &lo)) return 0;
+    if (!settle_piece(m2 - 1.0f, 1.33f / 6.0f, s2, t, maxt, &lo)) return 0;
+    if (!settle_piece(p.y, 0.83f / 6.0f, rd.y, t, maxt, &lo)) return 0;
     return 2.9f * lo >= 1.01f * res;
 }
 
@@ -448,7 +450,7 @@ static float softshadow2(const Ctx *C, vec3 ro, vec3 rd, float mint, float maxt,
     float ph = 1e20f;
     int it = 0;
     SettleRec *S = C->settle;
-    int settled = 0;
+    int settled = 0, step = 0;
     float res_at = 0.0f;
     if (S) S->marches++;
     for (float t = mint; t < maxt;) {
@@ -469,8 +471,8 @@ static float softshadow2(const Ctx *C, vec3 ro, vec3 rd, float mint, float maxt,
         if (S) {
             if (settled && res != res_at) S->violations++, res_at = res;
             vec3 pt = add(ro, muls(rd, t));
-            if (!settled && (C->scene == SCENE_T ? settle_test(C, pt, rd, t, maxt, res)
-                                                 : settle_test_O(C, pt, rd, t, maxt, res)))
+            if (!settled && ++step % S->every == 0 &&
+                (C->scene == SCENE_T ? settle_test(C, pt, rd, t, maxt, res) : settle_test_O(C, pt, rd, t, maxt, res)))
                 settled = 1, res_at = res, S->settled++;
         }
         t += h * 0.1f + 0.001f;
@@ -909,17 +911,19 @@ int oracle_render_pixels(int scene, const oracle_uniforms *u, int W, int H, cons
     return 0;
 }
 
-/* Soft-shadow settle analysis (analysis aid) over rows [row0, row0+nrows):
+/* Soft-shadow settle analysis (analysis aid) over rows [row0, row0+nrows),
+ * the rule tested on every `every`-th step of a march (the kernels' period):
  * out[5] = marches, steps, steps after the settle point, settled marches,
  * violations (res changed or occluded after settling). */
-int oracle_shadow_settle(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, uint64_t *out) {
-    if (!u || !out || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H) return 1;
+int oracle_shadow_settle(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, int every,
+                         uint64_t *out) {
+    if (!u || !out || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H || every < 1) return 1;
     uint64_t acc[5] = {0, 0, 0, 0, 0};
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < nrows; r++) {
         Ctx C;
         uint64_t cnt = 0;
-        SettleRec S = {0, 0, 0, 0, 0};
+        SettleRec S = {0, 0, 0, 0, 0, every};
         float px[4];
         init_ctx(&C, scene, u);
         C.evals = &cnt;

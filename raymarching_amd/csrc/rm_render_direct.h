@@ -160,18 +160,74 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
 #ifndef RM_SHADOW_P_PIN
 #define RM_SHADOW_P_PIN 1
 #endif
+// Scene O's settle rule (soft_shadow2_T_loop states it for
+// the sponge alone).  sceneSDF >= min(d0 - 0.33/6, d3 - 0.83/6, d1 - 1.33/6,
+// d2 - 1.33/6) (each sminCubic lowers a min by at most k/6; output_shader.frag:
+// 38-48 nests sphere d1 and cube d2, then the plane d3, then the sponge d0),
+// with d0 >= the sponge's box term and d2 >= the cube's Chebyshev term.  Each
+// of the four terms is convex along the ray (the plane linear), so it has an
+// affine minorant through its value and a subgradient at t; their minimum
+// minus the offsets, g, bounds every later h'.  If g >= 0.1 on [t, maxt]
+// (checked at both ends: affine) every later step is unoccluded and, sceneSDF
+// being 3-Lipschitz, h' / (2 ph) <= 0.665, so every later candidate is
+// >= 4 * 0.7469 g(t') / t'; each g_i / t' is monotonic, so the minimum is at t
+// or maxt: when 2.9 min(g(t) / t, g(maxt) / maxt) >= 1.01 res no later step
+// changes res.  res^2 = 16 num / den (squared, as the loop keeps it).
+// oracle settle_test_O restates the rule and checks it on every step of the
+// reference's marches.
+__device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& s, float t, float maxt, float num,
+                                                 float den) {
+    const float L = maxt - t;
+    const V3 p = at(w, t), q = at(s, t);
+    // sponge: box term in sponge space, slope along the sponge-space ray
+    const float qx = fabsf(q.x), qy = fabsf(q.y), qm = fmaxf(qx, fmaxf(qy, fabsf(q.z)));
+    const float sx = q.x < 0.0f ? -s.d.x : s.d.x, sy = q.y < 0.0f ? -s.d.y : s.d.y, sz = q.z < 0.0f ? -s.d.z : s.d.z;
+    const float s0 = qx == qm ? sx : qy == qm ? sy : sz;
+    const float a0 = qm - (1.0f + 0.33f / 6.0f);
+    // sphere (3,2,3) r 1: |e| - 1, slope e.d / |e|
+    const V3 e1 = p - v3(3.0f, 2.0f, 3.0f);
+    const float l1 = __builtin_amdgcn_sqrtf(dot(e1, e1));
+    const float a1 = l1 - (1.0f + 1.33f / 6.0f), s1 = dot(e1, w.d) * __builtin_amdgcn_rcpf(l1);
+    // cube (-5,4,5) r 1: Chebyshev term
+    const V3 e2 = p - v3(-5.0f, 4.0f, 5.0f);
+    const float bx = fabsf(e2.x), by = fabsf(e2.y), bm = fmaxf(bx, fmaxf(by, fabsf(e2.z)));
+    const float cx = e2.x < 0.0f ? -w.d.x : w.d.x, cy = e2.y < 0.0f ? -w.d.y : w.d.y, cz = e2.z < 0.0f ? -w.d.z : w.d.z;
+    const float s2 = bx == bm ? cx : by == bm ? cy : cz;
+    const float a2 = bm - (1.0f + 1.33f / 6.0f);
+    const float a3 = p.y - 0.83f / 6.0f;  // plane
+    const float g0 = fminf(fminf(a0, a1), fminf(a2, a3));
+    const float g1 = fminf(fminf(fmaf(s0, L, a0), fmaf(s1, L, a1)), fminf(fmaf(s2, L, a2), fmaf(w.d.y, L, a3)));
+    constexpr float K = (2.9f / 1.01f) * (2.9f / 1.01f) / 16.0f;
+    return (g0 >= 0.1f) & (g1 >= 0.1f) & (K * g0 * g0 * den >= num * t * t) & (K * g1 * g1 * den >= num * maxt * maxt);
+}
+
+#ifndef RM_SETTLE_O
+#define RM_SETTLE_O 1
+#endif
+#ifndef RM_SETTLE_O_EVERY
+#define RM_SETTLE_O_EVERY 8  // steps between settle tests (a power of 2)
+#endif
+
 // common.frag:810-831, k = 4, for scenes O/OG: the probes step along the
 // world ray and its sponge-space image, and the candidate is kept squared as
 // in soft_shadow2_T below (the shadow factor is smooth in its roundings).
-template <int SC>
+// SM as soft_shadow2_T_loop (0 none, 1 timed kernels: settle exit, 2
+// instrumented kernels: every step taken, those after the settle point counted
+// in cnt.skipped); O/OG only.  The settle test (~45 VALU) runs on every
+// RM_SETTLE_O_EVERY-th step: C5 frame 11.25 -> 10.51 ms with 8, 10.79 with 4
+// (profiles/r03/scene_O_settle_ab.jsonl).
+template <int SC, int SM = 0>
 __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
                                               Tally& cnt) {
+    constexpr bool kSettle = kPlaneSpans<SC> && SM != 0 && RM_SETTLE_O;
     const LinRay w{ro, rd}, s = sponge_ray(F, ro, rd);
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
     float t = mint;
     const float ia = plane_rate(rd);
     float t_plane = 0.0f;  // t < t_plane: sceneSDF is the floor plane (O/OG)
+    bool was_settled = false;  // SM == 2
     for (int it = 1; it == 1 ? t < maxt : true; it++) {
+        if constexpr (SM == 2) cnt.skipped += was_settled ? 1u : 0u;
         if constexpr (SC == SCENE_PLUGIN) {
             h = dist_probe<SC>(F, at(w, t), cnt);
         } else if (t < t_plane) {
@@ -191,12 +247,21 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
         bool upd = (Q >= 0.0f) & (cn * den < num * cd);
         num = upd ? cn : num;
         den = upd ? cd : den;
+        bool settled = false;
+        if constexpr (kSettle) {  // every RM_SETTLE_O_EVERY-th step (h >= 0.1 is implied by the rule; h >= ph: moving away)
+            if ((it & (RM_SETTLE_O_EVERY - 1)) == 0 && __builtin_amdgcn_ballot_w64((h >= 0.1f) & (h + h >= P)) != 0)
+                settled = (h >= 0.1f) & shadow_settled_O(w, s, t, maxt, num, den);
+        }
         P = h + h;
 #if RM_SHADOW_P_PIN
         asm volatile("" : "+v"(P));  // keep P's add in the step (not in a continue block of its own)
 #endif
         t += h * 0.1f + 0.001f;  // the reference's roundings: the step count is part of parity
-        if ((h < 0.001f) | !(t < maxt) | (it >= F.shadow_max_steps)) break;
+        if constexpr (SM == 2) {
+            was_settled |= settled;
+            settled = false;
+        }
+        if ((h < 0.001f) | !(t < maxt) | settled | (it >= F.shadow_max_steps)) break;
     }
     return h < 0.001f ? 0.0f : sqrtf(16.0f * num / den);
 }
@@ -234,6 +299,9 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // SM: 0 no settle test, 1 leave the march when settled (timed kernels), 2 run
 // the test and count the steps after it in cnt.skipped (instrumented kernels:
 // every reference step is still taken and counted)
+#ifndef RM_SETTLE_T_EVERY
+#define RM_SETTLE_T_EVERY 1  // steps between settle tests (a power of 2)
+#endif
 template <bool CAP, int NB, int SM = 0>
 __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                      Tally& cnt) {
@@ -258,7 +326,7 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
         den = upd ? cd : den;
         bool settled = false;
         if constexpr (SM != 0) {
-            if (__builtin_amdgcn_ballot_w64((box >= 0.1f) & (h + h >= P)) != 0) {
+            if ((it & (RM_SETTLE_T_EVERY - 1)) == 0 && __builtin_amdgcn_ballot_w64((box >= 0.1f) & (h + h >= P)) != 0) {
                 const float ax = fabsf(q.x), ay = fabsf(q.y), m = box + 1.0f;
                 const float sx = q.x < 0.0f ? -s.d.x : s.d.x, sy = q.y < 0.0f ? -s.d.y : s.d.y;
                 const float sz = q.z < 0.0f ? -s.d.z : s.d.z;
@@ -393,7 +461,7 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
 // output_shader.frag:127-176.  The material of the hit (the SdResult at mq)
 // is evaluated after the AO / shadow / thickness loops and returned in mat: it
 // is not live across them (16 floats fewer in registers during the loops).
-template <int SC>
+template <int SC, int SETTLE = 0>
 __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, V3 p, V3 n, V3 phongN, bool plane,
                                      Mat& mat, Tally& cnt) {
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
@@ -403,7 +471,7 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, 
 #ifdef RM_ABLATE_SHADOW
     float sha = 1.0f;
 #else
-    float sha = soft_shadow2<SC>(F, p, lightDir, 0.01f, length(Ld), cnt);
+    float sha = soft_shadow2<SC, SETTLE>(F, p, lightDir, 0.01f, length(Ld), cnt);
 #endif
 #ifdef RM_ABLATE_SSS
     float th = 0.5f;
@@ -434,7 +502,7 @@ __device__ __forceinline__ float fresnel(float n2, V3 normal, V3 incident, float
 }
 
 // output_shader.frag:246-262
-template <int SC>
+template <int SC, int SETTLE = 0>
 __device__ __forceinline__ V3 render_reflection(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
@@ -443,13 +511,13 @@ __device__ __forceinline__ V3 render_reflection(const FrameConst& F, V3 ro, V3 r
         V3 p = ro + rd * dist;
         const bool pl = plane_probes<SC>(F, p);
         V3 n = normal_fast<SC>(F, p, cnt, pl);
-        return light_O<SC>(F, q, ro, rd, p, n, n, pl, m, cnt);
+        return light_O<SC, SETTLE>(F, q, ro, rd, p, n, n, pl, m, cnt);
     }
     return background(ro, rd);
 }
 
 // output_shader.frag:298-343 (MAX_REFRACTIONS 4); live only in test scene OG
-template <int SC>
+template <int SC, int SETTLE = 0>
 __device__ __forceinline__ V3 render_refraction(const FrameConst& F, V3 ro, V3 rd, V3 absorption, Tally& cnt) {
     V3 color = v3s(0.0f);
     float invert = -1.0f;
@@ -468,7 +536,7 @@ __device__ __forceinline__ V3 render_refraction(const FrameConst& F, V3 ro, V3 r
         V3 g = normal_fast<SC>(F, p, cnt, pl);
         V3 n = g * invert;
         V3 ref = reflect(rd, n);
-        color = color + light_O<SC>(F, q, ro, ref, p, n, g, pl, m, cnt);
+        color = color + light_O<SC, SETTLE>(F, q, ro, ref, p, n, g, pl, m, cnt);
         if (invert > 0.0f) break;
         float ior = invert < 0.0f ? m.refraction_index : 1.0f / m.refraction_index;
         V3 raf = refract(rd, n, ior);
@@ -480,8 +548,8 @@ __device__ __forceinline__ V3 render_refraction(const FrameConst& F, V3 ro, V3 r
     return color * v3(expf(-absorption.x * absorb), expf(-absorption.y * absorb), expf(-absorption.z * absorb));
 }
 
-// output_shader.frag:348-385
-template <int SC>
+// output_shader.frag:348-385 (SETTLE: soft_shadow2's SM)
+template <int SC, int SETTLE = 0>
 __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     V3 q;
     float dist = cast_ray_d<SC, false>(F, ro, rd, q, cnt);
@@ -490,16 +558,16 @@ __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally&
     V3 p = ro + rd * dist;
     const bool pl = plane_probes<SC>(F, p);
     V3 n = normal_fast<SC>(F, p, cnt, pl);
-    V3 color = light_O<SC>(F, q, ro, rd, p, n, n, pl, m, cnt);
+    V3 color = light_O<SC, SETTLE>(F, q, ro, rd, p, n, n, pl, m, cnt);
     float rf = fresnel(m.refraction_index, n, rd, m.transparency > 0.0f ? 0.0f : m.reflectivity);
     if (m.reflectivity > 0.0f) {
         V3 r = reflect(rd, n);
-        color = color + (render_reflection<SC>(F, p + r * 0.001f, r, cnt) * rf) * m.reflectivity;
+        color = color + (render_reflection<SC, SETTLE>(F, p + r * 0.001f, r, cnt) * rf) * m.reflectivity;
     }
     if constexpr (SC == SCENE_OG || SC == SCENE_PLUGIN) {  // (scene O has no transparent material)
         if (m.transparency > 0.0f) {
             V3 r = refract(rd, n, 1.0f / m.refraction_index);
-            color = color + (render_refraction<SC>(F, p + r * 0.001f, r, m.absorption, cnt) * (1.0f - rf)) *
+            color = color + (render_refraction<SC, SETTLE>(F, p + r * 0.001f, r, m.absorption, cnt) * (1.0f - rf)) *
                                 m.transparency;
         }
     }
@@ -631,7 +699,7 @@ template <int SC, int NB = 3, int SETTLE = 0>
 __device__ __forceinline__ V3 render_pixel(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     if constexpr (SC == SCENE_S0) return render_S0(F, ro, rd, cnt);
     else if constexpr (SC == SCENE_T) return render_T<NB, SETTLE>(F, ro, rd, cnt);
-    else return render_O<SC>(F, ro, rd, cnt);  // O, OG and plugins: output_shader.frag's render()
+    else return render_O<SC, SETTLE>(F, ro, rd, cnt);  // O, OG and plugins: output_shader.frag's render()
 }
 
 // sceneSDF(p) of the scene at n points (rm_scene_eval): the distance in the
@@ -708,7 +776,7 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
             else c = render_pixel<SC, 3, COUNT ? 2 : 1>(F, ro, rd, cnt);
         } else {
             (void)lat;
-            c = render_pixel<SC>(F, ro, rd, cnt);
+            c = render_pixel<SC, 3, kPlaneSpans<SC> ? (COUNT ? 2 : 1) : 0>(F, ro, rd, cnt);
         }
         c = post_colour<FastMath<SC>::value>(c, vig);
         store_pixel(F, out, (size_t)j * F.W + x, c);

@@ -50,12 +50,13 @@ def main():
             print(p.stderr[-3000:])
             sys.exit(p.returncode)
         res.append(json.loads(p.stdout.strip().splitlines()[-1]))
-    ok = True
+    ok = all(v[3] for v in res[0].values())
+    print(json.dumps(dict(lib=os.path.basename(sys.argv[1]), timed_eq_instrumented=ok)))
     for lib, r in zip(sys.argv[2:], res[1:]):
         diff = [k for k in res[0] if r.get(k) != res[0][k]]
-        ok &= not diff
+        ok &= not diff and all(v[3] for v in r.values())
         print(json.dumps(dict(lib=os.path.basename(lib), vs=os.path.basename(sys.argv[1]), frames=len(r),
-                              identical=not diff, differ=diff)))
+                              identical=not diff, differ=diff, timed_eq_instrumented=all(v[3] for v in r.values()))))
     sys.exit(0 if ok else 1)
 
 
