@@ -309,9 +309,21 @@ __device__ __forceinline__ float menger_at(const LinRay& r, float t, Tally& n, b
     return menger<false, NB>(at(r, t), n.flop, active);
 }
 
-// sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4
+// sminCubic distance part (common.frag:72-80), k = vec2(k), k > 1e-4.
+// The probe form (!EXACT: AO, soft shadow, thickness, whose results are smooth
+// in the distance; m unused) is s = x^3 / (6 k^2) in three operations and the
+// closer distance as one IEEE minimum (the same value as aCloser ? a : b for
+// non-NaN distances): 7 VALU instead of 12 without contraction.
+#ifndef RM_SMIN_PROBE_FAST
+#define RM_SMIN_PROBE_FAST 1
+#endif
 template <bool EXACT>
 __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& m) {
+    if constexpr (!EXACT && RM_SMIN_PROBE_FAST) {
+        const float x = fmaxf(k - fabsf(a - b), 0.0f);
+        m = 0.0f;
+        return fmaf(-(x * x), x * (1.0f / (6.0f * k * k)), __builtin_elementwise_minimum(a, b));
+    }
     float x = fmaxf(k - fabsf(a - b), 0.0f);
     float h = EXACT ? div_const(x, k, 1.0f / k) : x * (1.0f / k);
     m = h * h * h * 0.5f;
