@@ -1155,7 +1155,14 @@ int oracle_mip_down(int w, int h, const uint32_t *in, uint32_t *out) {
     return 0;
 }
 
-/* bilinear fetch of a level (w x h) at normalized (u, v), CLAMP_TO_EDGE */
+/* bilinear fetch of a level (w x h) at normalized (u, v), CLAMP_TO_EDGE.
+ * The filter is evaluated as the polynomial of its cell, c00 + a Px + b (Py +
+ * a Pxy) with Px = c01 - c00, Py = c10 - c00, Pxy = (c11 - c10) - Px, in three
+ * fused multiply-adds per channel (GL leaves a filter's arithmetic to the
+ * implementation; SwiftShader filters unorm8 in fixed point, and this form
+ * stays within 1 LSB of its output, tests/test_bloom.py).  The HIP path
+ * (rm_post.hip) tabulates the same four coefficients per cell and evaluates
+ * the same three fmaf: bit-identical. */
 static vec3 tex_bilinear(const uint32_t *img, int w, int h, float u, float v) {
     float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
     float fx = floorf(x), fy = floorf(y);
@@ -1172,8 +1179,34 @@ static vec3 tex_bilinear(const uint32_t *img, int w, int h, float u, float v) {
         const int s = 8 * c;
         float c00 = (float)((t00 >> s) & 255u) * UNORM_K, c01 = (float)((t01 >> s) & 255u) * UNORM_K;
         float c10 = (float)((t10 >> s) & 255u) * UNORM_K, c11 = (float)((t11 >> s) & 255u) * UNORM_K;
-        float r0 = (1.0f - a) * c00 + a * c01, r1 = (1.0f - a) * c10 + a * c11;
-        o[c] = (1.0f - b) * r0 + b * r1;
+        const float px = c01 - c00, py = c10 - c00, pxy = (c11 - c10) - px;
+        o[c] = fmaf(b, fmaf(a, pxy, py), fmaf(a, px, c00));
+    }
+    return v3(o[0], o[1], o[2]);
+}
+
+/* One minified tap of a level accumulated into acc (the HIP path's order,
+ * rm_post.hip cell_acc): acc += g (c00 + a Px + b Py + a b Pxy) as
+ * acc += c00 g, Px (g a), Py (g b), Pxy (g a b), four fmaf per channel. */
+static vec3 bloom_tap_acc(const uint32_t *img, int w, int h, float u, float v, float g, vec3 acc) {
+    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    float fx = floorf(x), fy = floorf(y);
+    float a = x - fx, b = y - fy;
+    int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    x0 = x0 < 0 ? 0 : (x0 >= w ? w - 1 : x0);
+    x1 = x1 < 0 ? 0 : (x1 >= w ? w - 1 : x1);
+    y0 = y0 < 0 ? 0 : (y0 >= h ? h - 1 : y0);
+    y1 = y1 < 0 ? 0 : (y1 >= h ? h - 1 : y1);
+    const uint32_t t00 = img[(size_t)y0 * w + x0], t01 = img[(size_t)y0 * w + x1];
+    const uint32_t t10 = img[(size_t)y1 * w + x0], t11 = img[(size_t)y1 * w + x1];
+    const float ga = g * a, gb = g * b, gab = ga * b;
+    float o[3] = {acc.x, acc.y, acc.z};
+    for (int c = 0; c < 3; c++) {
+        const int s = 8 * c;
+        float c00 = (float)((t00 >> s) & 255u) * UNORM_K, c01 = (float)((t01 >> s) & 255u) * UNORM_K;
+        float c10 = (float)((t10 >> s) & 255u) * UNORM_K, c11 = (float)((t11 >> s) & 255u) * UNORM_K;
+        const float px = c01 - c00, py = c10 - c00, pxy = (c11 - c10) - px;
+        o[c] = fmaf(pxy, gab, fmaf(py, gb, fmaf(px, ga, fmaf(c00, g, o[c]))));
     }
     return v3(o[0], o[1], o[2]);
 }
@@ -1208,22 +1241,23 @@ static uint32_t bloom_pixel(const uint32_t *const *levels, const int *lw, const 
     const float u = tcx, v = 1.0f - tcy; /* bloom.frag:36 */
     vec3 color = tex_bilinear(levels[0], lw[0], lh[0], u, v);
     const float scale = 0.05f, iaspect = (float)H / (float)W, fr = lod - floorf(lod);
-    vec3 bl = v3(0.0f, 0.0f, 0.0f);
+    vec3 bl = v3(0.0f, 0.0f, 0.0f), b2 = v3(0.0f, 0.0f, 0.0f);
     for (int j = -2; j <= 2; j++)     /* bloom.frag:24-26 */
         for (int i = -2; i <= 2; i++) {
             const float uu = u + ((float)i * iaspect) * scale, vv = v + (float)j * scale;
-            vec3 s;
-            if (lod <= 0.0f) {
-                s = tex_bilinear(levels[0], lw[0], lh[0], uu, vv);
-            } else {
-                vec3 s1 = tex_bilinear(levels[d1], lw[d1], lh[d1], uu, vv);
-                vec3 s2 = tex_bilinear(levels[d2], lw[d2], lh[d2], uu, vv);
-                s = v3((1.0f - fr) * s1.x + fr * s2.x, (1.0f - fr) * s1.y + fr * s2.y,
-                       (1.0f - fr) * s1.z + fr * s2.z);
-            }
             const float g = G[abs(i)][abs(j)];
-            bl = v3(bl.x + g * s.x, bl.y + g * s.y, bl.z + g * s.z);
+            if (lod <= 0.0f) {
+                const vec3 s = tex_bilinear(levels[0], lw[0], lh[0], uu, vv);
+                bl = v3(fmaf(g, s.x, bl.x), fmaf(g, s.y, bl.y), fmaf(g, s.z, bl.z));
+            } else {
+                /* sum g ((1 - fr) s1 + fr s2) = (1 - fr) sum g s1 + fr sum g s2: the
+                 * Gaussian sums of the two levels, blended once at the end */
+                bl = bloom_tap_acc(levels[d1], lw[d1], lh[d1], uu, vv, g, bl);
+                b2 = bloom_tap_acc(levels[d2], lw[d2], lh[d2], uu, vv, g, b2);
+            }
         }
+    if (lod > 0.0f)
+        bl = v3((1.0f - fr) * bl.x + fr * b2.x, (1.0f - fr) * bl.y + fr * b2.y, (1.0f - fr) * bl.z + fr * b2.z);
     color = v3(color.x + gmax(bl.x - 0.3f, 0.0f), color.y + gmax(bl.y - 0.3f, 0.0f),
                color.z + gmax(bl.z - 0.3f, 0.0f)); /* bloom.frag:28,41 (intensity 1) */
     return unorm8(color.x) | (unorm8(color.y) << 8) | (unorm8(color.z) << 16) | (255u << 24);

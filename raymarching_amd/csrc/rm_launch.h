@@ -47,7 +47,7 @@ struct BloomPlan {
     int d1 = 0, d2 = 0;
     int w[40] = {}, h[40] = {};
     size_t offset[40] = {}, texels = 0;
-    size_t f4_offset = 0;  // lod > 0: levels d1, d2 as float4 (words from the buffer start)
+    size_t cell_offset = 0;  // lod > 0: the filter cells of levels d1, d2 (words from the buffer start)
 };
 BloomPlan bloom_plan(int W, int H);
 hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s);

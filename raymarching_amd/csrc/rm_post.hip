@@ -157,6 +157,13 @@ struct Level {
     int w, h;
 };
 
+// The bilinear filter as the polynomial of its cell (oracle tex_bilinear):
+// c00 + a Px + b (Py + a Pxy), Px = c01 - c00, Py = c10 - c00,
+// Pxy = (c11 - c10) - Px, three fused multiply-adds per channel.
+__device__ __forceinline__ float cell_poly(float c00, float px, float py, float pxy, float a, float b) {
+    return fmaf(b, fmaf(a, pxy, py), fmaf(a, px, c00));
+}
+
 // bilinear fetch at normalized (u, v), CLAMP_TO_EDGE, unorm8 -> c * (1/255)
 __device__ __forceinline__ RGB tex_bilinear(Level L, float u, float v) {
     const float x = u * (float)L.w - 0.5f, y = v * (float)L.h - 0.5f;
@@ -172,22 +179,22 @@ __device__ __forceinline__ RGB tex_bilinear(Level L, float u, float v) {
         const int s = 8 * c;
         const float c00 = (float)((t00 >> s) & 255u) * k, c01 = (float)((t01 >> s) & 255u) * k;
         const float c10 = (float)((t10 >> s) & 255u) * k, c11 = (float)((t11 >> s) & 255u) * k;
-        const float r0 = (1.0f - a) * c00 + a * c01, r1 = (1.0f - a) * c10 + a * c11;
-        o[c] = (1.0f - b) * r0 + b * r1;
+        const float px = c01 - c00, py = c10 - c00, pxy = (c11 - c10) - px;
+        o[c] = cell_poly(c00, px, py, pxy, a, b);
     }
     return RGB{o[0], o[1], o[2]};
 }
 
+__constant__ const float kGauss[3][3] = {{41.0f / 273.0f, 26.0f / 273.0f, 7.0f / 273.0f},
+                                         {26.0f / 273.0f, 16.0f / 273.0f, 4.0f / 273.0f},
+                                         {7.0f / 273.0f, 4.0f / 273.0f, 1.0f / 273.0f}};
+
 // bloom.frag:33-43, one lane per output pixel, 16x16-pixel workgroups.  The
 // general form: any lod, the levels read as RGBA8 words.  Used when lod <= 0
 // (magnification: every tap reads the base level).
-__global__ __launch_bounds__(256) void rm_bloom_kernel(Level L0, Level L1, Level L2, uint32_t* __restrict__ out,
-                                                       int W, int H, float lod, float fr) {
+__global__ __launch_bounds__(256) void rm_bloom_kernel(Level L0, uint32_t* __restrict__ out, int W, int H) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
-    const float G[3][3] = {{41.0f / 273.0f, 26.0f / 273.0f, 7.0f / 273.0f},
-                           {26.0f / 273.0f, 16.0f / 273.0f, 4.0f / 273.0f},
-                           {7.0f / 273.0f, 4.0f / 273.0f, 1.0f / 273.0f}};
     const float u = ((float)x + 0.5f) / (float)W, v = 1.0f - ((float)y + 0.5f) / (float)H;  // bloom.frag:36
     RGB color = tex_bilinear(L0, u, v);
     const float scale = 0.05f, iaspect = (float)H / (float)W;
@@ -197,185 +204,164 @@ __global__ __launch_bounds__(256) void rm_bloom_kernel(Level L0, Level L1, Level
 #pragma unroll
         for (int i = -2; i <= 2; i++) {
             const float uu = u + ((float)i * iaspect) * scale, vv = v + (float)j * scale;
-            RGB s;
-            if (lod <= 0.0f) {
-                s = tex_bilinear(L0, uu, vv);  // magnification: the base level
-            } else {
-                const RGB s1 = tex_bilinear(L1, uu, vv), s2 = tex_bilinear(L2, uu, vv);
-                s = RGB{(1.0f - fr) * s1.r + fr * s2.r, (1.0f - fr) * s1.g + fr * s2.g, (1.0f - fr) * s1.b + fr * s2.b};
-            }
-            const float g = G[i < 0 ? -i : i][j < 0 ? -j : j];
-            bl = RGB{bl.r + g * s.r, bl.g + g * s.g, bl.b + g * s.b};
+            const RGB s = tex_bilinear(L0, uu, vv);
+            const float g = kGauss[i < 0 ? -i : i][j < 0 ? -j : j];
+            bl = RGB{fmaf(g, s.r, bl.r), fmaf(g, s.g, bl.g), fmaf(g, s.b, bl.b)};
         }
     color = RGB{color.r + gmax_(bl.r - 0.3f, 0.0f), color.g + gmax_(bl.g - 0.3f, 0.0f),
                 color.b + gmax_(bl.b - 0.3f, 0.0f)};
     out[(size_t)y * W + x] = unorm8(color.r) | (unorm8(color.g) << 8) | (unorm8(color.b) << 16) | (255u << 24);
 }
 
-// The two minified levels bloom.frag reads, unpacked once to c * (1/255)
-// floats (the same product tex_bilinear forms per tap): RGB + pad.
-__global__ __launch_bounds__(256) void rm_level_f4_kernel(const uint32_t* __restrict__ a, int na,
-                                                          const uint32_t* __restrict__ b, int nb,
-                                                          float4* __restrict__ out) {
+// The cells of the two minified levels bloom.frag reads (lod > 0): for a
+// level of w x h texels, cell (cx, cy), cx in [-1, w-1], cy in [-1, h-1],
+// holds the filter polynomial of texels (clamp(cx), clamp(cx+1)) x (clamp(cy),
+// clamp(cy+1)) per channel: c00 rgb, Px rgb, Py rgb, Pxy rgb (12 floats,
+// 48 B; the same float operations tex_bilinear forms per tap).
+constexpr int kCellFloats = 12;
+__global__ __launch_bounds__(256) void rm_bloom_cells_kernel(const uint32_t* __restrict__ a, int wa, int ha,
+                                                             const uint32_t* __restrict__ b, int wb, int hb,
+                                                             float* __restrict__ cells) {
+    const int na = (wa + 1) * (ha + 1), nb = (wb + 1) * (hb + 1);
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= na + nb) return;
-    const uint32_t w = t < na ? a[t] : b[t - na];
-    const float k = 1.0f / 255.0f;
-    out[t] = make_float4((float)(w & 255u) * k, (float)((w >> 8) & 255u) * k, (float)((w >> 16) & 255u) * k, 0.0f);
+    const bool first = t < na;
+    const uint32_t* L = first ? a : b;
+    const int w = first ? wa : wb, h = first ? ha : hb, k = first ? t : t - na;
+    const int cx = k % (w + 1) - 1, cy = k / (w + 1) - 1;
+    const int x0 = clampi(cx, w - 1), x1 = clampi(cx + 1, w - 1), y0 = clampi(cy, h - 1), y1 = clampi(cy + 1, h - 1);
+    const uint32_t t00 = L[y0 * w + x0], t01 = L[y0 * w + x1], t10 = L[y1 * w + x0], t11 = L[y1 * w + x1];
+    const float kk = 1.0f / 255.0f;
+    float o[kCellFloats];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const int s = 8 * c;
+        const float c00 = (float)((t00 >> s) & 255u) * kk, c01 = (float)((t01 >> s) & 255u) * kk;
+        const float c10 = (float)((t10 >> s) & 255u) * kk, c11 = (float)((t11 >> s) & 255u) * kk;
+        o[c] = c00;
+        o[3 + c] = c01 - c00;
+        o[6 + c] = c10 - c00;
+        o[9 + c] = (c11 - c10) - o[3 + c];
+    }
+    float4* dst = reinterpret_cast<float4*>(cells + (size_t)t * kCellFloats);
+    dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+    dst[2] = make_float4(o[8], o[9], o[10], o[11]);
 }
 
-struct LevelF {
-    const float4* __restrict__ p;
-    int w, h;
+struct Cells {
+    const float* __restrict__ p;
+    int w, h;  // the level's texels; (w + 1) x (h + 1) cells
 };
 
-// One bilinear axis of a tap: weight and the two clamped texel indices.
-struct Axis {
+// One bilinear axis of a tap: weight and cell index (0 .. n: cx + 1).
+struct CAxis {
     float f;
-    int i0, i1;
-    bool uni;    // i0, i1 the same on every active lane of the wave
-    int so0, so1;  // when uni: i0, i1 times the axis' byte stride (wave-uniform)
+    int c;
 };
-
-__device__ __forceinline__ Axis axis(float t, int n, int stride) {
+__device__ __forceinline__ CAxis caxis(float t, int n) {
     const float x = t * (float)n - 0.5f, fx = floorf(x);
-    Axis A;
+    CAxis A;
     A.f = x - fx;
-    A.i0 = clampi((int)fx, n - 1);
-    A.i1 = clampi((int)fx + 1, n - 1);
-    const int f0 = __builtin_amdgcn_readfirstlane(A.i0), f1 = __builtin_amdgcn_readfirstlane(A.i1);
-    A.uni = __builtin_amdgcn_ballot_w64(A.i0 == f0 && A.i1 == f1) == __builtin_amdgcn_read_exec();
-    A.so0 = f0 * stride;
-    A.so1 = f1 * stride;
+    A.c = (int)fminf(fmaxf(fx, -1.0f), (float)(n - 1)) + 1;
     return A;
 }
-
-__device__ __forceinline__ RGB lerp2(float4 t00, float4 t01, float4 t10, float4 t11, float a, float b) {
-    const float ia = 1.0f - a, ib = 1.0f - b;
-    const float r0 = ia * t00.x + a * t01.x, r1 = ia * t10.x + a * t11.x;
-    const float g0 = ia * t00.y + a * t01.y, g1 = ia * t10.y + a * t11.y;
-    const float b0 = ia * t00.z + a * t01.z, b1 = ia * t10.z + a * t11.z;
-    return RGB{ib * r0 + b * r1, ib * g0 + b * g1, ib * b0 + b * b1};
+__device__ __forceinline__ bool wave_uniform(int v, int& first) {
+    first = __builtin_amdgcn_readfirstlane(v);
+    return __builtin_amdgcn_ballot_w64(v == first) == __builtin_amdgcn_read_exec();
 }
 
-// tex_bilinear over an unpacked level.  When both axes pick the same texels on
-// every lane (a wave is an 8x8-pixel tile; at 4096^2 a level texel spans 128+
-// pixels) the four texels are fetched once per wave through the scalar cache
-// into SGPRs; otherwise per lane.  Same floats, same operations either way.
-// Four float4 texels at wave-uniform byte offsets through the scalar cache
-// (read-only: the level was written by the previous launch on the stream).
-__device__ __forceinline__ void sload4(const float4* base, int o00, int o01, int o10, int o11, float4& t00, float4& t01,
-                                       float4& t10, float4& t11) {
+typedef float f8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+// Both levels' cells of one tap at wave-uniform byte offsets through the
+// scalar cache (read-only: written by the previous launch on the stream).
+__device__ __forceinline__ void sload_cells(const float* a, int oa, const float* b, int ob, f8v& a8, f4v& a4, f8v& b8,
+                                            f4v& b4) {
     asm volatile(
-        "s_load_dwordx4 %0, %4, %5\n\t"
-        "s_load_dwordx4 %1, %4, %6\n\t"
-        "s_load_dwordx4 %2, %4, %7\n\t"
-        "s_load_dwordx4 %3, %4, %8\n\t"
+        "s_load_dwordx8 %0, %4, %5\n\t"
+        "s_load_dwordx4 %1, %4, %5 offset:32\n\t"
+        "s_load_dwordx8 %2, %6, %7\n\t"
+        "s_load_dwordx4 %3, %6, %7 offset:32\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&s"(t00), "=&s"(t01), "=&s"(t10), "=&s"(t11)
-        : "s"(base), "s"(o00), "s"(o01), "s"(o10), "s"(o11)
+        : "=&s"(a8), "=&s"(a4), "=&s"(b8), "=&s"(b4)
+        : "s"(a), "s"(oa), "s"(b), "s"(ob)
         : "memory");
 }
 
-// Both levels' quads of one tap: eight loads in flight, one wait.
-__device__ __forceinline__ void sload8(const float4* a, int a00, int a01, int a10, int a11, const float4* b, int b00,
-                                       int b01, int b10, int b11, float4 (&t)[8]) {
-    asm volatile(
-        "s_load_dwordx4 %0, %8, %9\n\t"
-        "s_load_dwordx4 %1, %8, %10\n\t"
-        "s_load_dwordx4 %2, %8, %11\n\t"
-        "s_load_dwordx4 %3, %8, %12\n\t"
-        "s_load_dwordx4 %4, %13, %14\n\t"
-        "s_load_dwordx4 %5, %13, %15\n\t"
-        "s_load_dwordx4 %6, %13, %16\n\t"
-        "s_load_dwordx4 %7, %13, %17\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&s"(t[0]), "=&s"(t[1]), "=&s"(t[2]), "=&s"(t[3]), "=&s"(t[4]), "=&s"(t[5]), "=&s"(t[6]), "=&s"(t[7])
-        : "s"(a), "s"(a00), "s"(a01), "s"(a10), "s"(a11), "s"(b), "s"(b00), "s"(b01), "s"(b10), "s"(b11)
-        : "memory");
+// One tap of a level, accumulated: acc += g (c00 + a Px + b Py + a b Pxy) as
+// four multiply-adds per channel, acc += c00 g, Px (g a), Py (g b), Pxy (g a b)
+// in that order (oracle bloom_tap_acc): each reads one cell coefficient, so
+// the wave-uniform cells stay SGPR operands (one SGPR per VALU instruction).
+__device__ __forceinline__ void cell_acc(const f8v& c8, const f4v& c4, float a, float b, float g, RGB& acc) {
+    const float ga = g * a, gb = g * b, gab = ga * b;
+    acc.r = fmaf(c4[1], gab, fmaf(c8[6], gb, fmaf(c8[3], ga, fmaf(c8[0], g, acc.r))));
+    acc.g = fmaf(c4[2], gab, fmaf(c8[7], gb, fmaf(c8[4], ga, fmaf(c8[1], g, acc.g))));
+    acc.b = fmaf(c4[3], gab, fmaf(c4[0], gb, fmaf(c8[5], ga, fmaf(c8[2], g, acc.b))));
 }
-
-// Waterfall over the distinct texel quads of a tap that the wave's lanes need:
-// the first remaining lane's quad is fetched into SGPRs, the lanes that share
-// it interpolate and leave.
-__device__ __forceinline__ RGB tap_waterfall(const LevelF& L, const Axis& X, const Axis& Y) {
-    RGB r;
-    for (;;) {
-        const int x0 = __builtin_amdgcn_readfirstlane(X.i0), x1 = __builtin_amdgcn_readfirstlane(X.i1);
-        const int y0 = __builtin_amdgcn_readfirstlane(Y.i0), y1 = __builtin_amdgcn_readfirstlane(Y.i1);
-        if (X.i0 == x0 && X.i1 == x1 && Y.i0 == y0 && Y.i1 == y1) {
-            const int r0 = y0 * L.w, r1 = y1 * L.w;
-            float4 t00, t01, t10, t11;
-            sload4(L.p, __builtin_amdgcn_readfirstlane((r0 + x0) * 16), __builtin_amdgcn_readfirstlane((r0 + x1) * 16),
-                   __builtin_amdgcn_readfirstlane((r1 + x0) * 16), __builtin_amdgcn_readfirstlane((r1 + x1) * 16),
-                   t00, t01, t10, t11);
-            r = lerp2(t00, t01, t10, t11, X.f, Y.f);
-            break;
-        }
-    }
-    return r;
-}
-
-// One tap of bloom.frag:26 over levels A (d1) and B (d2), before the level
-// mix.  A wave is an 8x8-pixel tile and a level texel spans 2^d1 >= 0.025 H
-// pixels, so at frame sizes the wave's lanes nearly always share one texel
-// quad per level: both quads are fetched once into SGPRs and every lane
-// interpolates.  Otherwise the waterfall.  Same floats, same operations.
-__device__ __forceinline__ void tap2(const LevelF& A, const LevelF& B, const Axis& xa, const Axis& ya, const Axis& xb,
-                                     const Axis& yb, RGB& s1, RGB& s2) {
-    if (xa.uni && ya.uni && xb.uni && yb.uni) {
-        float4 t[8];
-        sload8(A.p, ya.so0 + xa.so0, ya.so0 + xa.so1, ya.so1 + xa.so0, ya.so1 + xa.so1, B.p, yb.so0 + xb.so0,
-               yb.so0 + xb.so1, yb.so1 + xb.so0, yb.so1 + xb.so1, t);
-        s1 = lerp2(t[0], t[1], t[2], t[3], xa.f, ya.f);
-        s2 = lerp2(t[4], t[5], t[6], t[7], xb.f, yb.f);
-    } else {
-        s1 = tap_waterfall(A, xa, ya);
-        s2 = tap_waterfall(B, xb, yb);
-    }
+__device__ __forceinline__ void vload_cell(const float* base, int cell, f8v& c8, f4v& c4) {
+    const float4* q = reinterpret_cast<const float4*>(base + (size_t)cell * kCellFloats);
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+    c8 = f8v{q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    c4 = f4v{q2.x, q2.y, q2.z, q2.w};
 }
 
 // bloom.frag:33-43 for lod > 0 (minification: levels d1, d2 blended by fr).
-// One wave per 8x8-pixel tile, 2x2 waves per workgroup.  The tap coordinates
-// depend on x or y alone, so the 10 column and 10 row axes are formed once per
-// lane (the general kernel forms them per tap: same values).
-// 5 waves per SIMD (<= 96 VGPRs, a 32-byte spill): hides more scalar-load latency than 4 (-4 %)
-#ifndef RM_BLOOM_WAVES
-#define RM_BLOOM_WAVES 5
-#endif
-__global__ __launch_bounds__(256, RM_BLOOM_WAVES) void rm_bloom_min_kernel(Level L0, LevelF A, LevelF B, uint32_t* __restrict__ out,
+// One wave per 8x8-pixel tile, 2x2 waves per workgroup.  A tap's value is
+// its cell's polynomial; a level texel spans 2^d1 >= 0.025 H pixels, so the
+// lanes of a wave nearly always share a tap's cell on both levels: the two
+// cells are fetched once per wave into SGPRs (otherwise per lane).  The
+// Gaussian sums of the two levels are blended once at the end (oracle
+// bloom_pixel).  31 VALU per tap.
+__global__ __launch_bounds__(256) void rm_bloom_min_kernel(Level L0, Cells A, Cells B, uint32_t* __restrict__ out,
                                                            int W, int H, float fr) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7), y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
     if (x >= W || y >= H) return;
-    const float G[3][3] = {{41.0f / 273.0f, 26.0f / 273.0f, 7.0f / 273.0f},
-                           {26.0f / 273.0f, 16.0f / 273.0f, 4.0f / 273.0f},
-                           {7.0f / 273.0f, 4.0f / 273.0f, 1.0f / 273.0f}};
     const float u = ((float)x + 0.5f) / (float)W, v = 1.0f - ((float)y + 0.5f) / (float)H;  // bloom.frag:36
     RGB color = tex_bilinear(L0, u, v);
     const float scale = 0.05f, iaspect = (float)H / (float)W;
-    Axis xa[5], xb[5];
+    CAxis xa[5], xb[5];
+    int sxa[5], sxb[5];
+    bool ux[5];
 #pragma unroll
-    for (int i = -2; i <= 2; i++) {
-        const float uu = u + ((float)i * iaspect) * scale;
-        xa[i + 2] = axis(uu, A.w, 16);
-        xb[i + 2] = axis(uu, B.w, 16);
+    for (int i = 0; i < 5; i++) {
+        const float uu = u + ((float)(i - 2) * iaspect) * scale;
+        xa[i] = caxis(uu, A.w);
+        xb[i] = caxis(uu, B.w);
+        const bool ua = wave_uniform(xa[i].c, sxa[i]), ub = wave_uniform(xb[i].c, sxb[i]);
+        ux[i] = ua && ub;
+        sxa[i] *= kCellFloats * 4;
+        sxb[i] *= kCellFloats * 4;
     }
-    RGB bl{0.0f, 0.0f, 0.0f};
+    RGB ba{0.0f, 0.0f, 0.0f}, bb{0.0f, 0.0f, 0.0f};
 #pragma unroll 1
-    for (int j = -2; j <= 2; j++) {  // rolled: keeps the tap addresses of one row live, not all 50
-        const float vv = v + (float)j * scale;
-        const Axis ya = axis(vv, A.h, 16 * A.w), yb = axis(vv, B.h, 16 * B.w);
-        const int aj = j < 0 ? -j : j;
+    for (int j = 0; j < 5; j++) {  // (rolled: one row's cells and weights live at a time)
+        const float vv = v + (float)(j - 2) * scale;
+        const CAxis ya = caxis(vv, A.h), yb = caxis(vv, B.h);
+        int sya, syb;
+        const bool uya = wave_uniform(ya.c, sya), uyb = wave_uniform(yb.c, syb);
+        const bool uy = uya && uyb;
+        sya *= (A.w + 1) * kCellFloats * 4;
+        syb *= (B.w + 1) * kCellFloats * 4;
 #pragma unroll
-        for (int i = -2; i <= 2; i++) {
-            RGB s1, s2;
-            tap2(A, B, xa[i + 2], ya, xb[i + 2], yb, s1, s2);
-            const RGB s{(1.0f - fr) * s1.r + fr * s2.r, (1.0f - fr) * s1.g + fr * s2.g, (1.0f - fr) * s1.b + fr * s2.b};
-            const float g = G[i < 0 ? -i : i][aj];
-            bl = RGB{bl.r + g * s.r, bl.g + g * s.g, bl.b + g * s.b};
+        for (int i = 0; i < 5; i++) {
+            const float g = kGauss[i < 2 ? 2 - i : i - 2][j < 2 ? 2 - j : j - 2];
+            f8v a8, b8;
+            f4v a4, b4;
+            if (uy & ux[i]) {  // (the arithmetic in each branch: SGPR operands stay SGPRs)
+                sload_cells(A.p, sya + sxa[i], B.p, syb + sxb[i], a8, a4, b8, b4);
+                cell_acc(a8, a4, xa[i].f, ya.f, g, ba);
+                cell_acc(b8, b4, xb[i].f, yb.f, g, bb);
+            } else {
+                vload_cell(A.p, ya.c * (A.w + 1) + xa[i].c, a8, a4);
+                vload_cell(B.p, yb.c * (B.w + 1) + xb[i].c, b8, b4);
+                cell_acc(a8, a4, xa[i].f, ya.f, g, ba);
+                cell_acc(b8, b4, xb[i].f, yb.f, g, bb);
+            }
         }
     }
+    const float ifr = 1.0f - fr;
+    const RGB bl{ifr * ba.r + fr * bb.r, ifr * ba.g + fr * bb.g, ifr * ba.b + fr * bb.b};
     color = RGB{color.r + gmax_(bl.r - 0.3f, 0.0f), color.g + gmax_(bl.g - 0.3f, 0.0f),
                 color.b + gmax_(bl.b - 0.3f, 0.0f)};
     out[(size_t)y * W + x] = unorm8(color.r) | (unorm8(color.g) << 8) | (unorm8(color.b) << 16) | (255u << 24);
@@ -403,9 +389,10 @@ BloomPlan bloom_plan(int W, int H) {
         p.offset[k] = p.texels;
         p.texels += (size_t)w * h;
     }
-    if (p.lod > 0.0f) {  // levels d1, d2 unpacked to float4, 16-byte aligned
-        p.f4_offset = (p.texels + 3) & ~(size_t)3;
-        p.texels = p.f4_offset + 4 * ((size_t)p.w[p.d1] * p.h[p.d1] + (size_t)p.w[p.d2] * p.h[p.d2]);
+    if (p.lod > 0.0f) {  // the cells of levels d1, d2 (rm_bloom_cells_kernel), 16-byte aligned
+        p.cell_offset = (p.texels + 3) & ~(size_t)3;
+        p.texels = p.cell_offset + (size_t)kCellFloats * ((size_t)(p.w[p.d1] + 1) * (p.h[p.d1] + 1) +
+                                                          (size_t)(p.w[p.d2] + 1) * (p.h[p.d2] + 1));
     }
     return p;
 }
@@ -423,15 +410,15 @@ hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const
     }
     const Level L0{in, W, H};
     if (p.lod <= 0.0f) {
-        hipLaunchKernelGGL(rm_bloom_kernel, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, L0, L0, L0, out, W, H,
-                           p.lod, p.fr);
+        hipLaunchKernelGGL(rm_bloom_kernel, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, L0, out, W, H);
         return hipGetLastError();
     }
-    const int na = p.w[p.d1] * p.h[p.d1], nb = p.w[p.d2] * p.h[p.d2];
-    float4* f4 = reinterpret_cast<float4*>(mips + p.f4_offset);
-    hipLaunchKernelGGL(rm_level_f4_kernel, dim3((na + nb + 255) / 256), dim3(256), 0, s, lv[p.d1], na, lv[p.d2], nb,
-                       f4);
-    const LevelF A{f4, p.w[p.d1], p.h[p.d1]}, B{f4 + na, p.w[p.d2], p.h[p.d2]};
+    const int wa = p.w[p.d1], ha = p.h[p.d1], wb = p.w[p.d2], hb = p.h[p.d2];
+    const int nc = (wa + 1) * (ha + 1) + (wb + 1) * (hb + 1);
+    float* cells = reinterpret_cast<float*>(mips + p.cell_offset);
+    hipLaunchKernelGGL(rm_bloom_cells_kernel, dim3((nc + 255) / 256), dim3(256), 0, s, lv[p.d1], wa, ha, lv[p.d2], wb,
+                       hb, cells);
+    const Cells A{cells, wa, ha}, B{cells + (size_t)kCellFloats * (wa + 1) * (ha + 1), wb, hb};
     hipLaunchKernelGGL(rm_bloom_min_kernel, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, L0, A, B, out, W, H,
                        p.fr);
     return hipGetLastError();
