@@ -314,6 +314,12 @@ __device__ __forceinline__ float menger_at(const LinRay& r, float t, Tally& n, b
 // in the distance; m unused) is s = x^3 / (6 k^2) in three operations and the
 // closer distance as one IEEE minimum (the same value as aCloser ? a : b for
 // non-NaN distances): 7 VALU instead of 12 without contraction.
+// RM_SMIN_EXACT_MINIMUM: the exact form's closer distance as one IEEE
+// minimum instead of compare + select (+ a hazard s_nop): C5 frame 9.89 ->
+// 9.59 ms, frames identical (profiles/r03/scene_O_micro_ab.jsonl)
+#ifndef RM_SMIN_EXACT_MINIMUM
+#define RM_SMIN_EXACT_MINIMUM 1
+#endif
 #ifndef RM_SMIN_PROBE_FAST
 #define RM_SMIN_PROBE_FAST 1
 #endif
@@ -328,7 +334,11 @@ __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& 
     float h = EXACT ? div_const(x, k, 1.0f / k) : x * (1.0f / k);
     m = h * h * h * 0.5f;
     float s = m * k * (1.0f / 3.0f);
+#if RM_SMIN_EXACT_MINIMUM  // (aCloser ? a : b) as one IEEE minimum: equal for non-NaN distances up to the sign of a zero
+    return __builtin_elementwise_minimum(a, b) - s;
+#else
     return (a < b ? a : b) - s;
+#endif
 }
 
 template <bool EXACT>
@@ -357,6 +367,9 @@ __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
 // margin over what exactness needs; rounding of the extrapolation is ~1e-5.
 // Callers use it to replace whole spans of rays and whole probe sets of a
 // shading point by the plane (PlaneSpan, rm_render_direct.h).
+#ifndef RM_O_LBS1  // C5 frame 10.22 -> 10.07 ms (profiles/r03/scene_O_micro_ab.jsonl)
+#define RM_O_LBS1 1
+#endif
 template <bool EXACT>
 __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n, float& slack) {
     n.evals++;
@@ -366,10 +379,16 @@ __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n, float& slack
     // distance, exactly also after rounding), and sminCubic lowers the min
     // by at most k/6: if even the bound of t1 is past the floor by more than
     // the blend width, t2 = sminCubic(t1, plane) is exactly the plane.
+#if RM_O_LBS1  // (one subtraction: the bounds decide branches with 0.01 of margin, never a value)
+    const float lbs = fminf(fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))),
+                            fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f)))) - 1.0834f;
+    n.flop += FL_BOUNDS + FL_BOX + 1;
+#else
     float lb1 = fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))) - 1.0f;
     float lb2 = fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f))) - 1.0f;
     n.flop += FL_BOUNDS + FL_BOX + 1;
     const float lbs = fminf(lb1, lb2) - 0.0834f;
+#endif
     const float mc = sponge_box(q);
     slack = fminf(lbs - (d3 + 0.51f), mc - (d3 + 0.34f));
     // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width

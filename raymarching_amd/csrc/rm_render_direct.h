@@ -204,6 +204,12 @@ __device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& 
 #ifndef RM_SETTLE_O
 #define RM_SETTLE_O 1
 #endif
+// RM_O_SHADOW_EXIT2: a settled lane leaves at the test, and the uniform step
+// cap is a branch of its own: the exit test no longer materializes four
+// booleans per step (C5 frame 10.22 -> 10.03 ms; profiles/r03/scene_O_micro_ab.jsonl)
+#ifndef RM_O_SHADOW_EXIT2
+#define RM_O_SHADOW_EXIT2 1
+#endif
 #ifndef RM_SETTLE_O_EVERY
 #define RM_SETTLE_O_EVERY 8  // steps between settle tests (a power of 2)
 #endif
@@ -251,6 +257,12 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
         if constexpr (kSettle) {  // every RM_SETTLE_O_EVERY-th step (h >= 0.1 is implied by the rule; h >= ph: moving away)
             if ((it & (RM_SETTLE_O_EVERY - 1)) == 0 && __builtin_amdgcn_ballot_w64((h >= 0.1f) & (h + h >= P)) != 0)
                 settled = (h >= 0.1f) & shadow_settled_O(w, s, t, maxt, num, den);
+#if RM_O_SHADOW_EXIT2
+            // (a settled lane leaves here: its result needs neither P nor t)
+            if constexpr (SM == 1) {
+                if (settled) break;
+            }
+#endif
         }
         P = h + h;
 #if RM_SHADOW_P_PIN
@@ -261,7 +273,12 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
             was_settled |= settled;
             settled = false;
         }
+#if RM_O_SHADOW_EXIT2
+        if ((h < 0.001f) | !(t < maxt)) break;
+        if (it >= F.shadow_max_steps) break;  // (wave-uniform)
+#else
         if ((h < 0.001f) | !(t < maxt) | settled | (it >= F.shadow_max_steps)) break;
+#endif
     }
     return h < 0.001f ? 0.0f : sqrtf(16.0f * num / den);
 }
@@ -299,6 +316,11 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // SM: 0 no settle test, 1 leave the march when settled (timed kernels), 2 run
 // the test and count the steps after it in cnt.skipped (instrumented kernels:
 // every reference step is still taken and counted)
+// RM_T_SHADOW_EXIT2: as RM_O_SHADOW_EXIT2 (C3 0.575 -> 0.568 ms, C2 P1
+// 0.192 -> 0.181)
+#ifndef RM_T_SHADOW_EXIT2
+#define RM_T_SHADOW_EXIT2 1
+#endif
 #ifndef RM_SETTLE_T_EVERY
 #define RM_SETTLE_T_EVERY 1  // steps between settle tests (a power of 2)
 #endif
@@ -337,6 +359,11 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
                           (K * be * be * den >= num * maxt * maxt);
             }
         }
+#if RM_T_SHADOW_EXIT2
+        if constexpr (SM == 1) {
+            if (settled) break;  // (the result needs neither P nor t)
+        }
+#endif
         P = h + h;
 #if RM_SHADOW_P_PIN
         asm volatile("" : "+v"(P));  // keep P's add in the step (not in a continue block of its own)
@@ -346,7 +373,12 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
             was_settled |= settled;
             settled = false;
         }
+#if RM_T_SHADOW_EXIT2
+        if ((h < 0.001f) | !(t < maxt)) break;
+        if (CAP && it >= F.shadow_max_steps) break;
+#else
         if ((h < 0.001f) | !(t < maxt) | settled | (CAP && it >= F.shadow_max_steps)) break;
+#endif
     }
     return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(16.0f * num * __builtin_amdgcn_rcpf(den));
 }
