@@ -183,17 +183,20 @@ def time_fxaa(r, frame8, stream, reps=20):
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": nbytes}
 
 
-BLOOM_FLOP_PER_TAP = 2 * 2 * 4 + 2 * 27 + 9 + 6 + 3  # axes, 2 bilinears, level mix, weighted sum, tap offset
-BLOOM_FLOP_PER_PX = 27 + 25 * BLOOM_FLOP_PER_TAP + 6      # + the base-level fetch and threshold/add
+# per tap and level: g a, g b, g a b and 12 multiply-adds (the cell polynomial
+# accumulated, rm_post.hip cell_acc); per pixel: 25 taps x 2 levels, the 20
+# bilinear axes (3 each) and 10 tap offsets (2), the base-level fetch (27), the
+# level blend (9), threshold and add (9)
+BLOOM_FLOP_PER_TAP = 2 * (3 + 2 * 12)
+BLOOM_FLOP_PER_PX = 25 * BLOOM_FLOP_PER_TAP + 20 * 3 + 10 * 2 + 27 + 9 + 9
 
 
 def time_bloom(r, frame8, stream, reps=20):
     """The reference's bloom pass (bloom.frag + its mip chain, main.cpp:212-214)
     over the RGBA8 frame on rank 0.  Its roofline is FP32 VALU: per pixel 25
-    taps x 2 trilinear levels of bilinear arithmetic (BLOOM_FLOP_PER_PX, every
-    op a separate mul/add: bloom.frag's rounding leaves no FMA), all texels
-    wave-uniform scalar loads.  HBM bytes (frame read twice, written once, mip
-    levels 1..d2 written and read once) are reported beside it."""
+    taps x 2 levels of the filter-cell polynomial (BLOOM_FLOP_PER_PX), the
+    cells wave-uniform scalar loads.  HBM bytes (frame read twice, written
+    once, mip levels 1..d2 written and read once) are reported beside it."""
     import math
 
     import torch
@@ -216,7 +219,7 @@ def time_bloom(r, frame8, stream, reps=20):
     tflops = W * H * BLOOM_FLOP_PER_PX / (ms / 1e3) / 1e12
     return {"name": "bloom (shaders/post/bloom.frag:14-43 + mip chain)", "ms": ms, "bound": "valu",
             "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": tflops / PEAK_FP32_TFLOPS,
-            "frac_of_non_fma_peak": tflops / (PEAK_FP32_TFLOPS / 2), "flop_per_px": BLOOM_FLOP_PER_PX,
+            "flop_per_px": BLOOM_FLOP_PER_PX,
             "hbm": {"achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
                     "algorithmic_bytes": nbytes},
             "mip_levels": d2, "texel_fetches_per_px": 4 * (1 + 25 * 2)}
