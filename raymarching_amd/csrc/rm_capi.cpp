@@ -276,11 +276,16 @@ int sched_period() {
 }
 
 // Dilation radius (tiles) of the sort key (rm_kernels.hip tile_key):
-// RM_SCHED_DILATE, default 0.
+// RM_SCHED_DILATE, default 2.  With a moving camera (bench.py --walk) the
+// costly regions move between the launch that measured the durations and
+// the launches that use the order: undilated, C3 walks at 0.457 ms per frame
+// against row-major's 0.440; radius 2 0.439, with the still pose unchanged
+// (0.583 ms, row-major 0.633); radius 4 0.437 walking but 0.589 still
+// (profiles/r03/sched_walk_dilate.jsonl).
 int sched_dilate() {
     static const int n = [] {
         const char *e = std::getenv("RM_SCHED_DILATE");
-        return e ? std::max(0, std::min(8, std::atoi(e))) : 0;
+        return e ? std::max(0, std::min(8, std::atoi(e))) : 2;
     }();
     return n;
 }

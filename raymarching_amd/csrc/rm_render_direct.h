@@ -175,6 +175,9 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
 // changes res.  res^2 = 16 num / den (squared, as the loop keeps it).
 // oracle settle_test_O restates the rule and checks it on every step of the
 // reference's marches.
+#ifndef RM_SETTLE_O_MIN  // (C5 frame 9.59 -> 9.56 ms, profiles/r03/scene_O_micro_ab.jsonl)
+#define RM_SETTLE_O_MIN 1
+#endif
 __device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& s, float t, float maxt, float num,
                                                  float den) {
     const float L = maxt - t;
@@ -198,7 +201,14 @@ __device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& 
     const float g0 = fminf(fminf(a0, a1), fminf(a2, a3));
     const float g1 = fminf(fminf(fmaf(s0, L, a0), fmaf(s1, L, a1)), fminf(fmaf(s2, L, a2), fmaf(w.d.y, L, a3)));
     constexpr float K = (2.9f / 1.01f) * (2.9f / 1.01f) / 16.0f;
+#if RM_SETTLE_O_MIN  // the four tests as one: IEEE minimum (NaN fails) of their margins >= 0
+    const float m = __builtin_elementwise_minimum(
+        __builtin_elementwise_minimum(__builtin_elementwise_minimum(g0, g1) - 0.1f, K * g0 * g0 * den - num * t * t),
+        K * g1 * g1 * den - num * maxt * maxt);
+    return m >= 0.0f;
+#else
     return (g0 >= 0.1f) & (g1 >= 0.1f) & (K * g0 * g0 * den >= num * t * t) & (K * g1 * g1 * den >= num * maxt * maxt);
+#endif
 }
 
 #ifndef RM_SETTLE_O
@@ -476,6 +486,9 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
     }
     float th = 0.0f;
     V3 nn = -norm;
+#ifdef RM_THICK_UNROLL
+#pragma unroll RM_THICK_UNROLL
+#endif
     for (int i = 0; i < 32; i++) {
         float fi = (float)i;
         float sl = F.hash11[i];

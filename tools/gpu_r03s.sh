@@ -1,0 +1,26 @@
+#!/bin/bash
+# round 3: end-of-change check: GPU suite, smoke(), bench lines (C3 still and
+# walking, C5 frame), kernel trace of the C3 bench
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/${OUTDIR:-r03s}
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+tail -3 $O/pytest.log
+[ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" $O/pytest.log | head -80; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 300 python bench.py > $O/bench_C3.json 2> $O/bench_C3.err || { tail -5 $O/bench_C3.err; exit 1; }
+timeout -k 10 300 python bench.py --walk --cpu-seconds 0 > $O/bench_C3_walk.json 2> $O/bench_C3_walk.err || { tail -5 $O/bench_C3_walk.err; exit 1; }
+timeout -k 10 300 python bench.py --scene O --size 8192 --max-steps 512 --steps 10 > $O/bench_C5.json 2> $O/bench_C5.err || { tail -5 $O/bench_C5.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --cpu-seconds 0 --steps 20 > $O/trace.log 2>&1 || { tail -5 $O/trace.log; exit 1; }
+find $O/trace -name "*kernel_stats.csv" -exec cp {} $O/bench_C3_kernel_stats.csv \;
+python - <<PY
+import json
+for f in ("bench_C3", "bench_C3_walk", "bench_C5"):
+    d = json.load(open("$O/" + f + ".json"))
+    print(f, "%.4g" % d["value"], "ms/step %.4f" % d["ms_per_step"], "kernel %.4f" % d["kernel_ms"], "frac %.3f" % d["roofline"]["frac"],
+          "cpu", d.get("cpu_baseline", {}).get("value"), "bloom", d.get("bloom_pass", {}).get("ms"))
+PY
+head -8 $O/bench_C3_kernel_stats.csv | cut -c1-160
