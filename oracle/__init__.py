@@ -193,12 +193,14 @@ def shadow_settle(scene: str, W: int, H: int, every: int = 1, **kw):
     every `every`-th step of the reference's shadow marches of a W x H frame
     (the kernels test scene O every 8th step, scene T every step) ->
     dict(marches, steps, after, settled, violations); `violations` counts
-    changes of res (or occlusions) after a march settled."""
+    changes of res (or occlusions) after a march settled, and scene-T
+    reflection marches past depth 3 whose clamp factor is not 1; `refl_after`
+    counts scene T's reflection-march steps begun at depth >= 3."""
     u = uniforms(W, H, **kw)
-    out = np.zeros(5, np.uint64)
+    out = np.zeros(6, np.uint64)
     if lib().oracle_shadow_settle(SCENES[scene], ctypes.byref(u), W, H, 0, H, every, out.ctypes.data):
         raise ValueError("oracle_shadow_settle failed")
-    return dict(zip(("marches", "steps", "after", "settled", "violations"), (int(v) for v in out)))
+    return dict(zip(("marches", "steps", "after", "settled", "violations", "refl_after"), (int(v) for v in out)))
 
 
 N_DIAG = 7

@@ -398,6 +398,7 @@ static vec3 phongContribForLight(vec3 k_d, vec3 k_s, float alpha, vec3 p, vec3 e
 typedef struct SettleRec {
     uint64_t marches, steps, after, settled, violations;
     int every; /* test on steps every, 2 every, ... of a march (1: every step) */
+    uint64_t refl_after; /* scene T: reflection-march steps begun at depth >= 3 */
 } SettleRec;
 static int settle_test(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, float res) {
     /* sponge space: q(t) = transformR(p - (0,3,0)), dq/dt = transformR(rd) (linear) */
@@ -536,11 +537,14 @@ static SdResult castRayDI(const Ctx *C, vec3 ro, vec3 rd) {
 }
 
 /* common.frag:931-954 */
-static vec3 castRay(const Ctx *C, vec3 ro, vec3 rd) {
+/* refl: the reflection march of getColorReflect (analysis: with C->settle,
+ * its steps begun at depth >= 3 are counted; rm_render_direct.h cast_ray_T RS) */
+static vec3 castRay(const Ctx *C, vec3 ro, vec3 rd, int refl) {
     seg_begin(C, PH_MARCH);
     float depth = ZNEAR;
     vec3 p = add(ro, muls(rd, depth));
     for (int i = 0; i < C->u.max_steps; i++) {
+        if (refl && C->settle && depth >= 3.0f) C->settle->refl_after++;
         float dist = sceneSDF(C, p).dist;
         if (dist < 0.001f) return p;
         depth += dist;
@@ -554,9 +558,13 @@ static vec3 castRay(const Ctx *C, vec3 ro, vec3 rd) {
  * `nr = getNormalFast(pr)` (:995) is dead code and is not evaluated. */
 static vec3 getColorReflect(const Ctx *C, vec3 p, vec3 n, vec3 rd) {
     vec3 reflect_dir = reflect3(rd, n);
-    vec3 pr = castRay(C, add(p, muls(reflect_dir, 0.01f)), reflect_dir);
+    SettleRec *S = C->settle;
+    const uint64_t before = S ? S->refl_after : 0;
+    vec3 pr = castRay(C, add(p, muls(reflect_dir, 0.01f)), reflect_dir, 1);
     vec3 c = v3s(1.0f);
     c = muls(c, gclamp(length3(sub(pr, p)) / 3.0f, 0.0f, 1.0f));
+    /* the rule: a march that went on past depth 3 ends with the factor 1 */
+    if (S && S->refl_after != before && c.x != 1.0f) S->violations++;
     return c;
 }
 
@@ -762,7 +770,7 @@ static vec3 render_O(const Ctx *C, vec3 ro, vec3 rd) {
 
 /* template.frag:45-76 */
 static vec3 render_T(const Ctx *C, vec3 ro, vec3 rd) {
-    vec3 p = castRay(C, ro, rd);
+    vec3 p = castRay(C, ro, rd, 0);
     vec3 n = getNormalFast(C, p);
     vec3 c = getColorReflect(C, p, n, rd);
     vec3 lightPos = v3(20.0f, 50.0f, 0.0f);
@@ -913,17 +921,19 @@ int oracle_render_pixels(int scene, const oracle_uniforms *u, int W, int H, cons
 
 /* Soft-shadow settle analysis (analysis aid) over rows [row0, row0+nrows),
  * the rule tested on every `every`-th step of a march (the kernels' period):
- * out[5] = marches, steps, steps after the settle point, settled marches,
- * violations (res changed or occluded after settling). */
+ * out[6] = marches, steps, steps after the settle point, settled marches,
+ * violations (res changed or occluded after settling; a scene-T reflection
+ * march past depth 3 whose clamp factor is not 1), scene T's reflection-march
+ * steps begun at depth >= 3 (the kernels' reflection stop). */
 int oracle_shadow_settle(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, int every,
                          uint64_t *out) {
     if (!u || !out || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H || every < 1) return 1;
-    uint64_t acc[5] = {0, 0, 0, 0, 0};
+    uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < nrows; r++) {
         Ctx C;
         uint64_t cnt = 0;
-        SettleRec S = {0, 0, 0, 0, 0, every};
+        SettleRec S = {0, 0, 0, 0, 0, every, 0};
         float px[4];
         init_ctx(&C, scene, u);
         C.evals = &cnt;
@@ -932,9 +942,10 @@ int oracle_shadow_settle(int scene, const oracle_uniforms *u, int W, int H, int 
 #pragma omp critical
         {
             acc[0] += S.marches; acc[1] += S.steps; acc[2] += S.after; acc[3] += S.settled; acc[4] += S.violations;
+            acc[5] += S.refl_after;
         }
     }
-    for (int i = 0; i < 5; i++) out[i] = acc[i];
+    for (int i = 0; i < 6; i++) out[i] = acc[i];
     return 0;
 }
 

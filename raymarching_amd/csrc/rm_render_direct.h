@@ -417,17 +417,28 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
 // depth of the point the reference returns (ZFAR on escape).  depth < ZFAR
 // holds at a hit and after step exhaustion, so the escape value is set once,
 // after the loop.
-template <int NB = 3>
+// RS, the reflection march of getColorReflect (common.frag:991-1002): its
+// point only enters the colour as clamp(length(pr - p) / 3, 0, 1), and depth
+// never decreases along the march, so once depth >= 3 (|pr - p| = 0.01 + depth
+// within 1e-5) that factor is 1 whatever the march does next.  RS = 1 (timed
+// kernels) leaves the march there; RS = 2 (instrumented) takes every step and
+// counts those after it in cnt.skipped.
+template <int NB = 3, int RS = 0>
 __device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s, Tally& cnt) {
+    constexpr float kStop = RS == 1 ? 3.0f : ZFAR;
     float depth = ZNEAR;
     for (int i = 0; i < F.max_steps; i++) {
+        if constexpr (RS == 2) cnt.skipped += depth >= 3.0f ? 1u : 0u;
         float dist = menger_at<NB>(s, depth, cnt);
         bool hit = dist < 0.001f;
         depth = hit ? depth : depth + dist;
-        if (hit | (depth >= ZFAR)) break;  // one exit test per step
+        if (hit | (depth >= kStop)) break;  // one exit test per step
     }
     return depth >= ZFAR ? ZFAR : depth;
 }
+#ifndef RM_REFLECT_STOP
+#define RM_REFLECT_STOP 1
+#endif
 
 // common.frag:850-866
 template <int SC, int NB = 3>
@@ -619,8 +630,9 @@ __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally&
     return color;
 }
 
-// template.frag:45-76 (scene T); NB: sponge_folds; SETTLE: soft_shadow2_T_loop
-template <int NB = 3, int SETTLE = 0>
+// template.frag:45-76 (scene T); NB: sponge_folds; SETTLE: soft_shadow2_T_loop;
+// RSTOP: cast_ray_T's RS for the reflection march
+template <int NB = 3, int SETTLE = 0, int RSTOP = 0>
 __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     constexpr int SC = SCENE_T;
     V3 p = ro + rd * cast_ray_T<NB>(F, sponge_ray(F, ro, rd), cnt);
@@ -631,7 +643,7 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
 #ifdef RM_ABLATE_REFLECT
     V3 pr = ror;
 #else
-    V3 pr = ror + rdir * cast_ray_T<NB>(F, sponge_ray(F, ror, rdir), cnt);
+    V3 pr = ror + rdir * cast_ray_T<NB, RM_REFLECT_STOP ? RSTOP : 0>(F, sponge_ray(F, ror, rdir), cnt);
 #endif
     float c = clamp01(length(pr - p) * (1.0f / 3.0f));
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
@@ -740,10 +752,10 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // SETTLE: the timed kernels' exact early exits (1), which the instrumented
 // (COUNT) kernels do not take but count (2): their ray-step counts and maps
 // stay the reference's, rm_stats.skipped the steps the timed kernels leave out
-template <int SC, int NB = 3, int SETTLE = 0>
+template <int SC, int NB = 3, int SETTLE = 0, int RSTOP = 0>
 __device__ __forceinline__ V3 render_pixel(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     if constexpr (SC == SCENE_S0) return render_S0(F, ro, rd, cnt);
-    else if constexpr (SC == SCENE_T) return render_T<NB, SETTLE>(F, ro, rd, cnt);
+    else if constexpr (SC == SCENE_T) return render_T<NB, SETTLE, RSTOP>(F, ro, rd, cnt);
     else return render_O<SC, SETTLE>(F, ro, rd, cnt);  // O, OG and plugins: output_shader.frag's render()
 }
 
@@ -817,8 +829,8 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
             // (no settle exit in the latency tiles: their long grazing shadow marches
             // settle late or never, and the test lengthens the lone waves that end
             // the launch: C4 share +16 %, C2 P1 +12 % with it)
-            if (lat) c = render_pixel<SC, 1, 0>(F, ro, rd, cnt);
-            else c = render_pixel<SC, 3, COUNT ? 2 : 1>(F, ro, rd, cnt);
+            if (lat) c = render_pixel<SC, 1, 0, COUNT ? 2 : 1>(F, ro, rd, cnt);
+            else c = render_pixel<SC, 3, COUNT ? 2 : 1, COUNT ? 2 : 1>(F, ro, rd, cnt);
         } else {
             (void)lat;
             c = render_pixel<SC, 3, kPlaneSpans<SC> ? (COUNT ? 2 : 1) : 0>(F, ro, rd, cnt);
