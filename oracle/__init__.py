@@ -195,12 +195,15 @@ def shadow_settle(scene: str, W: int, H: int, every: int = 1, **kw):
     dict(marches, steps, after, settled, violations); `violations` counts
     changes of res (or occlusions) after a march settled, and scene-T
     reflection marches past depth 3 whose clamp factor is not 1; `refl_after`
-    counts scene T's reflection-march steps begun at depth >= 3."""
+    counts scene T's reflection-march steps begun at depth >= 3, `back_steps`
+    the shadow-march steps of points facing away from the light (`after`
+    counts the other marches' steps only)."""
     u = uniforms(W, H, **kw)
-    out = np.zeros(6, np.uint64)
+    out = np.zeros(7, np.uint64)
     if lib().oracle_shadow_settle(SCENES[scene], ctypes.byref(u), W, H, 0, H, every, out.ctypes.data):
         raise ValueError("oracle_shadow_settle failed")
-    return dict(zip(("marches", "steps", "after", "settled", "violations", "refl_after"), (int(v) for v in out)))
+    return dict(zip(("marches", "steps", "after", "settled", "violations", "refl_after", "back_steps"),
+                    (int(v) for v in out)))
 
 
 N_DIAG = 7

@@ -399,6 +399,8 @@ typedef struct SettleRec {
     uint64_t marches, steps, after, settled, violations;
     int every; /* test on steps every, 2 every, ... of a march (1: every step) */
     uint64_t refl_after; /* scene T: reflection-march steps begun at depth >= 3 */
+    int back;            /* the current march shades a point facing away from the light */
+    uint64_t back_steps; /* steps of such marches (their result is multiplied by 0) */
 } SettleRec;
 static int settle_test(const Ctx *C, vec3 p, vec3 rd, float t, float maxt, float res) {
     /* sponge space: q(t) = transformR(p - (0,3,0)), dq/dt = transformR(rd) (linear) */
@@ -459,7 +461,8 @@ static float softshadow2(const Ctx *C, vec3 ro, vec3 rd, float mint, float maxt,
         float h = sceneSDF(C, add(ro, muls(rd, t))).dist;
         if (S) {
             S->steps++;
-            if (settled) S->after++;
+            if (S->back) S->back_steps++;
+            else if (settled) S->after++;
         }
         if (h < 0.001f) {
             if (S && settled) S->violations++;
@@ -649,7 +652,9 @@ static vec3 light(const Ctx *C, const Material *mat, vec3 ro, vec3 rd, vec3 p, v
     vec3 lightPos = v3(20.0f, 50.0f, 0.0f);
     vec3 lightDir = normalize3(sub(lightPos, p));
     float occ = ambientOcclusionReal(C, p, n);
+    if (C->settle) C->settle->back = dot3(normalize3(sub(lightPos, p)), phongN) < 0.0f;
     float sha = softshadow2(C, p, lightDir, 0.01f, length3(sub(lightPos, p)), 4.0f);
+    if (C->settle) C->settle->back = 0;
     float sky = gclamp(0.5f + 0.5f * n.y, 0.0f, 1.0f);
     float ind = gclamp(dot3(n, normalize3(mul(lightDir, v3(-1.0f, 0.0f, -1.0f)))), 0.0f, 1.0f);
     vec3 shading = phongContribForLight(v3(1.64f, 1.27f, 0.99f), mat->specular, mat->shininess, p, ro,
@@ -776,7 +781,9 @@ static vec3 render_T(const Ctx *C, vec3 ro, vec3 rd) {
     vec3 lightPos = v3(20.0f, 50.0f, 0.0f);
     vec3 lightDir = normalize3(sub(lightPos, p));
     float occ = ambientOcclusionReal(C, p, n);
+    if (C->settle) C->settle->back = dot3(normalize3(sub(lightPos, p)), n) < 0.0f;
     float sha = softshadow2(C, p, lightDir, 0.01f, length3(sub(lightPos, p)), 4.0f);
+    if (C->settle) C->settle->back = 0;
     float sky = gclamp(0.5f + 0.5f * n.y, 0.0f, 1.0f);
     float ind = gclamp(dot3(n, normalize3(mul(lightDir, v3(-1.0f, 0.0f, -1.0f)))), 0.0f, 1.0f);
     float fre = powf(gclamp(1.0f + dot3(n, rd), 0.0f, 1.0f), 2.0f);
@@ -921,19 +928,22 @@ int oracle_render_pixels(int scene, const oracle_uniforms *u, int W, int H, cons
 
 /* Soft-shadow settle analysis (analysis aid) over rows [row0, row0+nrows),
  * the rule tested on every `every`-th step of a march (the kernels' period):
- * out[6] = marches, steps, steps after the settle point, settled marches,
+ * out[7] = marches, steps, steps after the settle point, settled marches,
  * violations (res changed or occluded after settling; a scene-T reflection
  * march past depth 3 whose clamp factor is not 1), scene T's reflection-march
- * steps begun at depth >= 3 (the kernels' reflection stop). */
+ * steps begun at depth >= 3 (the kernels' reflection stop), the shadow-march
+ * steps of points facing away from the light (phong's dotLN < 0: the shadow
+ * factor multiplies 0; the kernels skip these marches).  Settle steps are
+ * counted for the other marches only. */
 int oracle_shadow_settle(int scene, const oracle_uniforms *u, int W, int H, int row0, int nrows, int every,
                          uint64_t *out) {
     if (!u || !out || W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H || every < 1) return 1;
-    uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < nrows; r++) {
         Ctx C;
         uint64_t cnt = 0;
-        SettleRec S = {0, 0, 0, 0, 0, every, 0};
+        SettleRec S = {0, 0, 0, 0, 0, every, 0, 0, 0};
         float px[4];
         init_ctx(&C, scene, u);
         C.evals = &cnt;
@@ -943,9 +953,10 @@ int oracle_shadow_settle(int scene, const oracle_uniforms *u, int W, int H, int 
         {
             acc[0] += S.marches; acc[1] += S.steps; acc[2] += S.after; acc[3] += S.settled; acc[4] += S.violations;
             acc[5] += S.refl_after;
+            acc[6] += S.back_steps;
         }
     }
-    for (int i = 0; i < 6; i++) out[i] = acc[i];
+    for (int i = 0; i < 7; i++) out[i] = acc[i];
     return 0;
 }
 

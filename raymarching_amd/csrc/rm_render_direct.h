@@ -456,10 +456,10 @@ __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tall
     return sum / maxSum;
 }
 
-// common.frag:730-754 (N = the caller's normal)
+// common.frag:730-754 (N = the caller's normal; L = normalize(lightPos - p),
+// the caller's light direction, the same value)
 template <int SC>
-__device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 p, V3 eye, V3 lightPos, V3 N) {
-    V3 L = mnormalize<SC>(lightPos - p);
+__device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 L, V3 p, V3 eye, V3 N) {
     V3 V = mnormalize<SC>(eye - p);
     V3 R = mnormalize<SC>(reflect(-L, N));
     float dotLN = dot(L, N);
@@ -467,6 +467,33 @@ __device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 p, V3 eye, V
     if (dotLN < 0.0f) return v3s(0.0f);
     if (dotRV < 0.0f) return k_d * dotLN;
     return k_d * dotLN + k_s * mpow<SC>(dotRV, alpha);
+}
+
+// Soft shadows of points facing away from the light: phong returns 0 when
+// dot(L, N) < 0 (common.frag:742), and the shadow factor only multiplies
+// phong's term, by shadow_pow(sha), finite for any sha in [0, 1]: the product
+// is 0 whatever the march returns.  SM 1 (timed kernels) skips the march
+// (sha = 1), SM 2 (instrumented) takes it and counts its steps in
+// cnt.skipped, SM 0 takes it.  dotLN is phong's own dot(L, N): the same
+// value, so the same decision.  Scene T at P0: 54 % of the shadow-march steps
+// (oracle shadow_settle back_steps), scene O 0-6 % (its floor faces the light).
+#ifndef RM_BACKFACE_SKIP
+#define RM_BACKFACE_SKIP 1
+#endif
+template <int SM, typename March>
+__device__ __forceinline__ float shadow_if_lit(float dotLN, Tally& cnt, March march) {
+    const bool lit = !(dotLN < 0.0f);
+    if constexpr (SM == 1 && RM_BACKFACE_SKIP) {
+        return lit ? march() : 1.0f;
+    } else {
+        const uint32_t e0 = cnt.evals, s0 = cnt.skipped;
+        const float sha = march();
+        if constexpr (SM == 2 && RM_BACKFACE_SKIP) {
+            if (!lit) cnt.skipped = s0 + (cnt.evals - e0);
+        }
+        (void)e0; (void)s0; (void)lit;
+        return sha;
+    }
 }
 
 template <int SC>
@@ -527,7 +554,9 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, 
 #ifdef RM_ABLATE_SHADOW
     float sha = 1.0f;
 #else
-    float sha = soft_shadow2<SC, SETTLE>(F, p, lightDir, 0.01f, length(Ld), cnt);
+    float sha = shadow_if_lit<SETTLE>(dot(lightDir, phongN), cnt, [&] {
+        return soft_shadow2<SC, SETTLE>(F, p, lightDir, 0.01f, length(Ld), cnt);
+    });
 #endif
 #ifdef RM_ABLATE_SSS
     float th = 0.5f;
@@ -538,7 +567,7 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, 
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     V3 shading =
-        phong<SC>(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, p, ro, lightPos, phongN) * shadow_pow<SC>(sha);
+        phong<SC>(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, lightDir, p, ro, phongN) * shadow_pow<SC>(sha);
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
     V3 sssl = lightDir + n * 0.6f;
@@ -654,14 +683,16 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
 #ifdef RM_ABLATE_SHADOW
     float sha = 1.0f;
 #else
-    float sha = soft_shadow2_T<NB, SETTLE>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
+    float sha = shadow_if_lit<RSTOP>(dot(lightDir, n), cnt, [&] {
+        return soft_shadow2_T<NB, SETTLE>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
+    });
 #endif
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     float fre = clamp01(1.0f + dot(n, rd));
     fre = fre * fre;  // pow(x, 2.0)
     V3 shading =
-        phong<SC>(v3(1.64f, 1.27f, 0.99f), v3(1.0f, 1.0f, 0.0f), 1280.0f, p, ro, lightPos, n) * shadow_pow<SC>(sha);
+        phong<SC>(v3(1.64f, 1.27f, 0.99f), v3(1.0f, 1.0f, 0.0f), 1280.0f, lightDir, p, ro, n) * shadow_pow<SC>(sha);
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
     shading = shading + v3s(fre * occ);
