@@ -470,8 +470,9 @@ __device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 L, V3 p, V3 
 }
 
 // Soft shadows of points facing away from the light: phong returns 0 when
-// dot(L, N) < 0 (common.frag:742), and the shadow factor only multiplies
-// phong's term, by shadow_pow(sha), finite for any sha in [0, 1]: the product
+// dot(L, N) < 0 (common.frag:738-745), and the shadow factor only multiplies
+// phong's term (template.frag:58,66; output_shader.frag:133,148),
+// by shadow_pow(sha), finite for any sha in [0, 1]: the product
 // is 0 whatever the march returns.  SM 1 (timed kernels) skips the march
 // (sha = 1), SM 2 (instrumented) takes it and counts its steps in
 // cnt.skipped, SM 0 takes it.  dotLN is phong's own dot(L, N): the same
