@@ -831,6 +831,9 @@ template <> struct Tiling<KERNEL_PERSIST> : Tiling<KERNEL_TILE8> {};
 // evals[0..2] (ray-steps, FLOP, ray-steps the timed kernels skip).
 // (bx, by): the tile's position in dispatch order on a gx-wide tile grid
 // (blockIdx for the hardware-dispatched kernels).
+#ifndef RM_LAT_SETTLE
+#define RM_LAT_SETTLE 0
+#endif
 template <int SC, bool COUNT, int K, typename OUT>
 __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restrict__ out,
                                                unsigned long long* __restrict__ evals, int bx, int by, int gx) {
@@ -861,7 +864,7 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
             // (no settle exit in the latency tiles: their long grazing shadow marches
             // settle late or never, and the test lengthens the lone waves that end
             // the launch: C4 share +16 %, C2 P1 +12 % with it)
-            if (lat) c = render_pixel<SC, 1, 0, COUNT ? 2 : 1>(F, ro, rd, cnt);
+            if (lat) c = render_pixel<SC, 1, RM_LAT_SETTLE ? (COUNT ? 2 : 1) : 0, COUNT ? 2 : 1>(F, ro, rd, cnt);
             else c = render_pixel<SC, 3, COUNT ? 2 : 1, COUNT ? 2 : 1>(F, ro, rd, cnt);
         } else {
             (void)lat;
