@@ -440,14 +440,26 @@ __device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s
 #define RM_REFLECT_STOP 1
 #endif
 
-// common.frag:850-866
+// common.frag:850-866.  Scene O rolls the probe loop: the unrolled loop's
+// interleaved probes spilled 18 VGPRs of the 8-wave kernel to scratch, rolled
+// 4 (same frames, C5 frame 9.46 -> 9.43 ms; scene T's rolled loop measured
+// 3 % slower, profiles/r03/rolled_probes_ab.jsonl)
+#ifndef RM_AO_ROLLED_O
+#define RM_AO_ROLLED_O 1
+#endif
 template <int SC, int NB = 3>
 __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tally& cnt, bool plane = false) {
     float sum = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
+    auto probe = [&](int i) {
         V3 p = pos + (n * (float)(i + 1)) * 0.2f;
         sum += (1.0f / (float)(1 << i)) * dist_at<SC, false, NB>(F, p, cnt, plane);
+    };
+    if constexpr (kPlaneSpans<SC> && RM_AO_ROLLED_O) {
+#pragma unroll 1
+        for (int i = 0; i < 4; i++) probe(i);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) probe(i);
     }
     // maxSum = sum_i 2^-i (i+1) 0.2, accumulated in f32 as the reference does
     float maxSum = 0.0f;
