@@ -435,7 +435,8 @@ def main():
             },
             "value_note": "value counts the reference's ray-steps (sceneSDF calls of common.frag's loops) per "
                           "frame; the kernels leave out steps that provably cannot change the frame (exact early "
-                          "exits: settled soft shadows, DESIGN.md 2.11), so they execute "
+                          "exits: settled soft shadows, the shadows of points facing away from the light, scene "
+                          "T's reflection march past depth 3; DESIGN.md 2.11-2.13), so they execute "
                           "executed_ray_steps_per_s; frames_per_s is the same either way",
             "executed_ray_steps_per_s": (evals_frame - skipped_frame) * args.steps / elapsed,
             "kernel_ms": kern, "kernel_ms_max_rank": kern_max, "frame_stream_ms": frame_stream_ms,

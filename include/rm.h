@@ -68,8 +68,9 @@ typedef struct rm_stats {
                         exits skip Menger folds and scene O's primitives)          */
     uint64_t skipped; /* when count_evals: of `evals`, the ray-steps the uninstrumented
                         kernels do not execute (exact early exits whose results equal
-                        the reference's: scene T's settled soft shadows, DESIGN.md
-                        2.11); executed = evals - skipped                            */
+                        the reference's: settled soft shadows, the soft shadows of
+                        points facing away from the light, scene T's reflection march
+                        past depth 3); executed = evals - skipped */
 } rm_stats;
 
 /* Create a context on HIP device `device`.  Scene unset, params default. */
