@@ -44,7 +44,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R
         V3 ro, rd;
         camera_ray<false>(F, x, y, tcx, tcy, ro, rd);
         const float vig = vignette<false>(tcx, tcy);
-        V3 c = post_colour<false>(render_pixel<SCENE_PLUGIN>(F, ro, rd, cnt), vig);
+        // the exact skips of scene O's pipeline that hold for any scene (the soft
+        // shadows of points facing away from the light): taken
+        // by the timed launches, counted by the instrumented ones
+        V3 c = evals ? render_pixel<SCENE_PLUGIN, 3, 2>(F, ro, rd, cnt) : render_pixel<SCENE_PLUGIN, 3, 1>(F, ro, rd, cnt);
+        c = post_colour<false>(c, vig);
         const size_t i = (size_t)j * F.W + x;
         if (rgba8) store_pixel(F, static_cast<uint32_t*>(out), i, c);
         else store_pixel(F, static_cast<float4*>(out), i, c);
@@ -55,10 +59,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R
     }
     if (evals) {
         if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;
-        uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop);
+        uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop), ss = wave_sum_u32(cnt.skipped);
         if (lane == 0) {
             atomicAdd(&evals[0], (unsigned long long)se);
             atomicAdd(&evals[1], (unsigned long long)sf);
+            if (ss) atomicAdd(&evals[2], (unsigned long long)ss);
         }
     }
 }
