@@ -262,15 +262,18 @@ int lat_tiles() {
     return n;
 }
 
-// Launches per dispatch-order sort of a geometry (rm_ctx::Sched): 4 -- an
-// order is at most 5 launches old (frame-to-frame coherence keeps it good), and
-// the duration stores, the sort and the cross-stream events run on one launch
-// in four (C3 frame 0.683 -> 0.672 ms).  RM_SCHED_PERIOD
-// overrides it (1 = re-sort after every launch).
+// Launches per dispatch-order sort of a geometry (rm_ctx::Sched): 8 -- an
+// order is at most 9 launches old (frame-to-frame coherence keeps it good, the
+// dilated key covers a moving camera), and the duration stores, the sort and
+// the cross-stream events run on one launch in eight.  Round 2 chose 4 (C3
+// frame 0.683 -> 0.672 ms against 1); after the round-3 skips the frame is
+// shorter and 8 measured 0.7 % (still) and 1.8 % (walking) faster than 4, 16
+// the same as 8 (profiles/r03/sched_period_after_skips.jsonl).
+// RM_SCHED_PERIOD overrides it (1 = re-sort after every launch).
 int sched_period() {
     static const int n = [] {
         const char *e = std::getenv("RM_SCHED_PERIOD");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 8;
     }();
     return n;
 }
