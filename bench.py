@@ -361,12 +361,21 @@ def main():
     torch.cuda.synchronize(dev)
 
     nch = len(fr.cuts) - 1
+    # frame-stream interval: with one frame stream and one chunk, one event pair
+    # on that stream around the whole timed region (per-frame timing events
+    # cost 2 % of a C3 frame: 0.481 -> 0.471 ms without them,
+    # profiles/r03/bench_events_ab.jsonl); otherwise a pair around each render
+    whole = len(fr.streams) == 1 and nch == 1
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nch)]
-           for _ in range(args.steps)]
+           for _ in range(1 if whole else args.steps)]
+    if whole:
+        evs[0][0][0].record(fr.streams[0])
     t0 = time.perf_counter()
     for i in range(args.steps):
         set_frame(i)
-        fr.submit(events=evs[i])  # frame i's gather overlaps frame i+1's render
+        fr.submit(events=None if whole else evs[i])  # frame i's gather overlaps frame i+1's render
+    if whole:
+        evs[0][0][1].record(fr.streams[0])
     fr.flush()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -377,7 +386,10 @@ def main():
     live = [c for c in range(nch) if min(fr.cuts[c + 1], fr.nmine) > fr.cuts[c]]  # chunks with rows here
     # per-frame interval of the render calls on the frame stream (events around each call: the render
     # kernel plus the dispatch-order sort it enqueues; with 2 streams it also spans overlapping frames)
-    frame_stream_ms = sum(evs[i][c][0].elapsed_time(evs[i][c][1]) for i in range(args.steps) for c in live) / args.steps
+    if whole:
+        frame_stream_ms = evs[0][0][0].elapsed_time(evs[0][0][1]) / args.steps if live else 0.0
+    else:
+        frame_stream_ms = sum(evs[i][c][0].elapsed_time(evs[i][c][1]) for i in range(args.steps) for c in live) / args.steps
     # per-launch render-kernel duration (the roofline denominator): synchronous launches of this rank's
     # rows on the frames' stream, HIP events around the kernel alone (rm_stats.kernel_ms), after the
     # timed region
