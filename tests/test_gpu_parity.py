@@ -782,13 +782,15 @@ def test_persistent_waves_equal_hardware_dispatch(R, torch_cuda, scene):
 @pytest.mark.parametrize("scene,pose", [("T", p) for p in POSES] + [("O", p) for p in POSES] +
                          [("OG", p) for p in ("P0", "P3", "P7")])
 def test_settled_soft_shadows_keep_pixels(R, torch_cuda, scene, pose):
-    """The timed kernels of scenes T, O and OG leave a soft-shadow march once no
-    later step can change it (O/OG test the rule every 8th
-    step); the instrumented kernel takes every reference step and counts the
+    """The timed kernels of scenes T, O and OG leave out the ray-steps that
+    cannot change the frame: a soft-shadow march once settled (DESIGN.md 2.11;
+    O/OG test the rule every 8th step), scene T's reflection march past depth 3
+    (2.12), and the whole soft shadow of a point facing away from the light
+    (2.13).  The instrumented kernel takes every reference step and counts the
     ones left out (rm_stats.skipped).  The timed frame (row-major and ordered,
     float4 and RGBA8) equals the instrumented frame bit for bit, the step map
     stays the reference's, and the share of steps left out is the oracle's
-    share of steps after the settle point, within 2 %."""
+    (shadow_settle: after + refl_after + back_steps), within 2 %."""
     torch = torch_cuda
     steps = 128 if scene == "T" else 512
     setup(R, scene, POSES[pose], steps)
