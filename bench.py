@@ -163,6 +163,36 @@ def cpu_baseline(args, pose, W, H, target_s):
     }
 
 
+def frame_check(r, frame, W, H, fmt):
+    """The last timed frame (rank 0's whole frame: de-interleaved for N > 1)
+    against one render of the same pose by the instrumented kernel
+    (count_evals=1: every reference ray-step, the kernel the parity tests check
+    against the oracle).  The timed kernels leave out steps that cannot change
+    the frame (common.frag:810-831, :931-954, :991-1002),
+    so the two frames must be the same bits; anything else fails the run."""
+    import torch
+
+    timed = frame.clone()
+    r.set_params(count_evals=1)
+    ref = r.render_rgba8(W, H) if fmt == "rgba8" else r.render(W, H)
+    r.set_params(count_evals=0)
+    torch.cuda.synchronize()
+    diff = (timed.view(torch.int32) != ref.view(torch.int32)).reshape(H * W, -1).any(-1)
+    nd = int(diff.sum())
+    res = {"result": "bit-exact" if nd == 0 else "MISMATCH", "pixels": W * H, "pixels_differing": nd,
+           "against": "one render of the last timed pose by the instrumented kernel (count_evals=1, every "
+                      "reference ray-step), " + ("RGBA8 words" if fmt == "rgba8" else "float4 bits")}
+    if nd:
+        print(json.dumps({"frame_check": res}), file=sys.stderr, flush=True)
+        raise SystemExit(f"frame_check: {nd} of {W * H} pixels of the timed frame differ from the instrumented frame")
+    return res
+
+
+def _median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2]
+
+
 def time_fxaa(r, frame8, stream, reps=20):
     """The reference's FXAA pass (post.frag) over the RGBA8 frame on rank 0:
     HBM-bound stencil, 4 B read + 4 B written per pixel (algorithmic)."""
@@ -383,6 +413,8 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+    # the last timed frame against the instrumented kernel's frame of the same pose (rank 0)
+    check = frame_check(r, fr.frame, W, H, args.fmt) if rank == 0 else None
     live = [c for c in range(nch) if min(fr.cuts[c + 1], fr.nmine) > fr.cuts[c]]  # chunks with rows here
     # per-frame interval of the render calls on the frame stream (events around each call: the render
     # kernel plus the dispatch-order sort it enqueues; with 2 streams it also spans overlapping frames)
@@ -397,7 +429,32 @@ def main():
     launch = sorted(fr.render_local(stats=True)[1]["kernel_ms"] for _ in range(11)) if fr.nmine else [0.0]
     kern = launch[len(launch) // 2]
     kt = torch.tensor([kern], dtype=torch.float64, device=red_dev)
+    exchange = None
     if world > 1:
+        # the frame's steps one at a time (render, pack, gather, de-interleave),
+        # each timed alone after the timed region: the gather's own time, which
+        # the pipelined frames overlap with the next frame's render
+        xs = [fr.timed_exchange() for _ in range(5)]
+        mine = torch.tensor([kern] + [_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
+                                                                                "deinterleave_ms")],
+                            dtype=torch.float64, device=red_dev)
+        per_rank = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+        pr = [[float(v) for v in x.cpu()] for x in per_rank]
+        exchange = {
+            "gather_ms": pr[0][3], "deinterleave_ms": pr[0][4], "pack_ms": pr[0][2],
+            "kernel_ms_per_rank": [x[0] for x in pr], "gather_ms_per_rank": [x[3] for x in pr],
+            "pack_ms_per_rank": [x[2] for x in pr],
+            "wire_bytes_per_rank": fr.wires[0].numel() * fr.wires[0].element_size(),
+            "root_ingress_bytes": (world - 1) * fr.wires[0].numel() * fr.wires[0].element_size(),
+            "backend": args.backend,
+            "note": "median of 5 frames whose steps run one after another, each timed alone after the timed "
+                    "region: kernel_ms_per_rank = each rank's render kernel (11 synchronous launches), "
+                    "pack = RGBA8 -> 3 B/px wire, gather = the transfer alone (all ranks packed before it "
+                    "starts; HIP events around the RCCL gather, wall time of the host-staged gather with gloo), "
+                    "deinterleave = rank 0's de-interleave kernel; the timed frames pipeline frame k's gather "
+                    "and de-interleave with frame k+1's render",
+        }
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
     elapsed, kern_max = float(t.item()), float(kt.item())
@@ -457,7 +514,10 @@ def main():
                               "timed frames); frame_stream_ms = mean interval of the timed frames' render calls "
                               "(kernel + dispatch-order sort; with 2 streams it spans overlapping frames)",
             "roofline": roof,
+            "frame_check": check,
         }
+        if exchange is not None:
+            res.update(exchange)
         if fr.frame is not None and fr.fmt == "rgba8":
             res["post_pass"] = time_fxaa(r, fr.frame, stream)
             res["bloom_pass"] = time_bloom(r, fr.frame, stream)

@@ -33,6 +33,15 @@
 extern "C" {
 #endif
 
+/* Version of the structs and calls below.  Bumped whenever a struct the
+ * library writes grows or a call changes meaning; a caller compiled against
+ * one version must not pass its structs to a library of another (check
+ * rm_abi_version() == RM_ABI_VERSION once at start-up).
+ *   1  round 1-2 (rm_stats without `skipped`)
+ *   2  rm_stats.skipped
+ *   3  rm_stats.dispatch, rm_stats.lat_tiles; rm_abi_version() */
+#define RM_ABI_VERSION 3
+
 typedef enum rm_status {
     RM_OK = 0,
     RM_ERR_INVALID_ARGUMENT = 1, /* bad pointer/size/uniform arity                       */
@@ -54,9 +63,17 @@ typedef struct rm_params {
                                  4 8x8 px tiles pulled by persistent waves from an atomic counter (built-in scenes) */
     int32_t schedule;         /* dispatch order of one-wave tiles: 1 (default) = the costliest tiles of a recent
                                  launch of the same geometry on the same stream first (their measured durations,
-                                 counting-sorted on the GPU after every 4th launch, RM_SCHED_PERIOD); 0 = row-major.
+                                 counting-sorted on the GPU after every 8th launch, RM_SCHED_PERIOD; the first two
+                                 launches of a geometry run row-major); 0 = row-major.
                                  Pixels are the same either way; an rm_set_tile_order order takes precedence. */
 } rm_params;
+
+/* rm_stats.dispatch: the order the launch's workgroups rendered tiles in */
+enum {
+    RM_DISPATCH_ROW_MAJOR = 0, /* workgroup i renders tile i                                    */
+    RM_DISPATCH_EXPLICIT = 1,  /* rm_set_tile_order's order                                      */
+    RM_DISPATCH_ADAPTIVE = 2   /* sorted durations of an earlier launch (rm_params.schedule = 1)  */
+};
 
 typedef struct rm_stats {
     uint64_t evals;  /* sceneSDF calls (ray-steps) of this render, when count_evals   */
@@ -71,7 +88,18 @@ typedef struct rm_stats {
                         the reference's: settled soft shadows, the soft shadows of
                         points facing away from the light, scene T's reflection march
                         past depth 3); executed = evals - skipped */
+    int32_t dispatch; /* RM_DISPATCH_*: the tile order this launch ran (ABI 3)           */
+    int32_t lat_tiles; /* scene T: workgroups that rendered with the latency-optimized
+                         fold tests (the costliest tiles at the head of an ordered
+                         launch); 0 otherwise (ABI 3)                   */
+    float gather_ms;   /* rm_render_sharded*: device time of the RGB8 pack and the gather
+                         on this rank's stream (rank 0: until every wire has arrived,
+                         so it includes waiting for the slowest rank); 0 elsewhere (ABI 3) */
+    float deinterleave_ms; /* rm_render_sharded*, rank 0: the de-interleave kernel (ABI 3) */
 } rm_stats;
+
+/* RM_ABI_VERSION of the library (compare with the header's). */
+int rm_abi_version(void);
 
 /* Create a context on HIP device `device`.  Scene unset, params default. */
 rm_status rm_create(rm_ctx **out, int device);
@@ -255,7 +283,8 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
  * One process driving n GPUs: rm_comm_init_all over n contexts on distinct
  * devices (ncclCommInitAll; comms[i] is rank i), then rm_render_sharded_all.
  * Calls are asynchronous on the contexts' streams unless `stats` is given
- * (then they wait; stats[i].kernel_ms is rank i's render time). */
+ * (then they wait; stats[i].kernel_ms is rank i's render time, gather_ms its
+ * pack + gather and, on rank 0, deinterleave_ms the de-interleave kernel). */
 typedef struct rm_comm rm_comm;
 typedef struct rm_comm_id {
     char internal[128]; /* an ncclUniqueId */

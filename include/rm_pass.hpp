@@ -35,6 +35,13 @@ public:
     enum Type { Fragment };
 
     explicit Shader(int device = 0) : device_(device) {
+        // a librm.so of another ABI would read and write these structs with
+        // other layouts (include/rm.h RM_ABI_VERSION)
+        if (rm_abi_version() != RM_ABI_VERSION) {
+            std::fprintf(stderr, "rm::Shader: librm.so has ABI %d, rm.h declares %d\n", rm_abi_version(),
+                         RM_ABI_VERSION);
+            return;
+        }
         if (rm_create(&ctx_, device) != RM_OK) ctx_ = nullptr;
     }
     ~Shader() {
@@ -112,9 +119,10 @@ public:
                RM_OK;
     }
     Format format() const { return fmt_; }
-    // the device target: RGBA8 words (R in the low byte) or RGBA32F texels
-    uint32_t* textureRGBA8() { return fmt_ == RGBA8 ? static_cast<uint32_t*>(tex_) : nullptr; }
-    float* texture() { return fmt_ == RGBA32F ? static_cast<float*>(tex_) : nullptr; }
+    // the device target: RGBA8 words (R in the low byte) or RGBA32F texels;
+    // asking for the other format's view returns null and says so once
+    uint32_t* textureRGBA8() { return fmt_ == RGBA8 ? static_cast<uint32_t*>(tex_) : mismatch<uint32_t>("RGBA8"); }
+    float* texture() { return fmt_ == RGBA32F ? static_cast<float*>(tex_) : mismatch<float>("RGBA32F"); }
     int width() const { return w_; }
     int height() const { return h_; }
     // RGBA8 (the reference target's format), row 0 first (looks up).  An
@@ -136,6 +144,15 @@ public:
     }
 
 private:
+    template <typename T>
+    T* mismatch(const char* want) {
+        if (!warned_) {
+            std::fprintf(stderr, "rm::RenderTexture: a %s view of a %s target (create(w, h, RenderTexture::%s))\n",
+                         want, fmt_ == RGBA8 ? "RGBA8" : "RGBA32F", want);
+            warned_ = true;
+        }
+        return nullptr;
+    }
     void release() {
         if (tex_) (void)hipFree(tex_);
         if (packed_) (void)hipFree(packed_);
@@ -146,6 +163,7 @@ private:
     uint32_t* packed_ = nullptr;
     int w_ = 0, h_ = 0;
     Format fmt_ = RGBA8;
+    bool warned_ = false;
 };
 
 // The multi-GPU form of RenderTexture::draw: a W x H RGBA8 frame whose row

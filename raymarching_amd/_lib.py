@@ -25,7 +25,11 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_render_rgba8", "rm_render_accumulate", "rm_render_accumulate_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_last_error", "rm_status_string",
            "rm_compile_scene", "rm_scene_eval", "rm_render_step_map", "rm_sharded_layout", "rm_comm_get_id",
            "rm_comm_init_rank", "rm_comm_init_all", "rm_comm_destroy", "rm_render_sharded", "rm_render_sharded_all",
-           "rm_set_tile_order", "rm_tile_grid", "rm_comm_info")
+           "rm_set_tile_order", "rm_tile_grid", "rm_comm_info", "rm_abi_version")
+
+# include/rm.h RM_ABI_VERSION: the struct layouts below
+ABI_VERSION = 3
+DISPATCH = {0: "row-major", 1: "explicit", 2: "adaptive"}
 
 
 class RmParams(ctypes.Structure):
@@ -35,11 +39,15 @@ class RmParams(ctypes.Structure):
 
 class RmStats(ctypes.Structure):
     _fields_ = [("evals", ctypes.c_uint64), ("pixels", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
-                ("scene", ctypes.c_int32), ("flop", ctypes.c_uint64), ("skipped", ctypes.c_uint64)]
+                ("scene", ctypes.c_int32), ("flop", ctypes.c_uint64), ("skipped", ctypes.c_uint64),
+                ("dispatch", ctypes.c_int32), ("lat_tiles", ctypes.c_int32), ("gather_ms", ctypes.c_float),
+                ("deinterleave_ms", ctypes.c_float)]
 
     def as_dict(self):
         return dict(evals=int(self.evals), pixels=int(self.pixels), kernel_ms=float(self.kernel_ms),
-                    scene=int(self.scene), flop=int(self.flop), skipped=int(self.skipped))
+                    scene=int(self.scene), flop=int(self.flop), skipped=int(self.skipped),
+                    dispatch=DISPATCH.get(int(self.dispatch), int(self.dispatch)), lat_tiles=int(self.lat_tiles),
+                    gather_ms=float(self.gather_ms), deinterleave_ms=float(self.deinterleave_ms))
 
 
 class RmShardLayout(ctypes.Structure):
@@ -121,6 +129,7 @@ def lib() -> ctypes.CDLL:
                                   c.c_int),
         "rm_set_tile_order": ([vp, vp, c.c_int64], c.c_int),
         "rm_tile_grid": ([c.POINTER(RmParams), c.c_int, c.c_int, c.POINTER(c.c_int), c.POINTER(c.c_int)], c.c_int),
+        "rm_abi_version": ([], c.c_int),
         "rm_last_error": ([vp], cp),
         "rm_status_string": ([c.c_int], cp),
     }
@@ -128,6 +137,9 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    v = L.rm_abi_version()
+    if v != ABI_VERSION:  # a stale build: its structs differ from the ones bound here
+        raise ImportError(f"{LIB_PATH} has ABI version {v}, this binding expects {ABI_VERSION}; rebuild it")
     _LIB = L
     return L
 

@@ -39,10 +39,26 @@ struct rm_ctx {
     float pos[3] = {0.0f, 0.0f, 0.0f};
     float mouse[2] = {0.0f, 0.0f};
     float time = 0.0f;
-    // KERNEL_PERSIST: one block of self-resetting tile counters per stream the
-    // context launched on (launches on one stream run one after another, so a
-    // block is never shared by two launches in flight)
-    std::vector<std::pair<hipStream_t, uint32_t *>> persist;
+    // KERNEL_PERSIST: blocks of self-resetting tile counters, one per stream
+    // the context launches on (launches on one stream run one after another, so
+    // a block is never shared by two launches in flight).  At most kPersistBlocks:
+    // a new stream takes the least recently used block once the event recorded
+    // after its last launch has completed (the launch left its counters zeroed).
+    struct PersistBlock {
+        hipStream_t stream = nullptr;
+        uint32_t *ctr = nullptr;
+        hipEvent_t last = nullptr;
+        uint64_t used = 0;
+    };
+    static constexpr int kPersistBlocks = 4;
+    std::vector<PersistBlock> persist;
+    // work this context enqueued: `done` is recorded after each call that
+    // enqueues on `stream`; when the stream changes, the previous one's event
+    // is kept in `retired` until it completes (rm_destroy waits for these and
+    // the side stream instead of the whole device)
+    hipEvent_t done = nullptr;
+    bool done_recorded = false;
+    std::vector<hipEvent_t> retired;
     float sample_part = 1.0f;  // u_sample_part, u_seed1, u_seed2: read by rm_render_accumulate*
     float seed1[2] = {0.0f, 0.0f}, seed2[2] = {0.0f, 0.0f};
     rm_params params = {128, 0, 0, 0, 1};
@@ -97,6 +113,40 @@ rm_status hip_fail(rm_ctx *c, hipError_t e, const char *what) {
         hipError_t e_ = (call);                               \
         if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
     } while (0)
+
+// Record that the context enqueued work on its stream (rm_ctx::done).
+rm_status mark_done(rm_ctx *ctx) {
+    RM_HIP(hipEventRecord(ctx->done, ctx->stream));
+    ctx->done_recorded = true;
+    return RM_OK;
+}
+
+// The KERNEL_PERSIST counter block of the ctx stream (rm_ctx::PersistBlock).
+rm_status persist_block(rm_ctx *ctx, rm_ctx::PersistBlock *&out) {
+    static uint64_t clock = 0;
+    out = nullptr;
+    for (auto &b : ctx->persist)
+        if (b.stream == ctx->stream) out = &b;
+    if (!out && (int)ctx->persist.size() < rm_ctx::kPersistBlocks) {
+        ctx->persist.emplace_back();
+        rm_ctx::PersistBlock &b = ctx->persist.back();
+        const size_t bytes = (size_t)rm::kPersistWords * sizeof(uint32_t);
+        RM_HIP(hipEventCreateWithFlags(&b.last, hipEventDisableTiming));
+        RM_HIP(hipMalloc(&b.ctr, bytes));
+        RM_HIP(hipMemsetAsync(b.ctr, 0, bytes, ctx->stream));
+        b.stream = ctx->stream;
+        out = &b;
+    }
+    if (!out) {  // recycle the least recently used block once its last launch is done
+        out = &ctx->persist[0];
+        for (auto &b : ctx->persist)
+            if (b.used < out->used) out = &b;
+        RM_HIP(hipEventSynchronize(out->last));
+        out->stream = ctx->stream;
+    }
+    out->used = ++clock;
+    return RM_OK;
+}
 
 // ShaderLoader::preprocess (source/shader_loader.cpp:22-81): read the file
 // line by line; a line holding "#include" not preceded by "//" pulls in the
@@ -434,7 +484,12 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         if (st != RM_OK) return st;
         if (sc) {
             const uint64_t P = (uint64_t)sched_period(), k = sc->k;
-            if (k % P == 0) F.tile_cost = sc->buf + ((k / P) & 1) * sc->n;  // sort k / P reads them
+            // an instrumented launch (count_evals, step maps) takes every reference
+            // step, so its tile durations would rank the tiles by work the timed
+            // kernels skip: it uses the current order but records no durations and
+            // does not advance the geometry's launch count
+            if (k % P == 0 && !(ctx->params.count_evals != 0 || evmap))
+                F.tile_cost = sc->buf + ((k / P) & 1) * sc->n;  // sort k / P reads them
             if (k >= 2) {  // the newest order whose sort had a launch to overlap
                 const uint64_t s = (k - 2) / P;
                 if (k - 2 == s * P) RM_HIP(hipStreamWaitEvent(ctx->stream, sc->sorted[s & 1], 0));
@@ -442,18 +497,12 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
             }
         }
     }
+    rm_ctx::PersistBlock *pb = nullptr;
     if (ctx->scene != rm::SCENE_PLUGIN && pick_kernel(ctx) == rm::KERNEL_PERSIST) {
         // this stream's counters, zeroed once; each launch leaves them zeroed
-        for (auto &sp : ctx->persist)
-            if (sp.first == ctx->stream) F.persist = sp.second;
-        if (!F.persist) {
-            const size_t bytes = (size_t)rm::kPersistWords * sizeof(uint32_t);
-            uint32_t *blk = nullptr;
-            RM_HIP(hipMalloc(&blk, bytes));
-            ctx->persist.emplace_back(ctx->stream, blk);
-            RM_HIP(hipMemsetAsync(blk, 0, bytes, ctx->stream));
-            F.persist = blk;
-        }
+        rm_status st = persist_block(ctx, pb);
+        if (st != RM_OK) return st;
+        F.persist = pb->ctr;
     }
     bool cnt = ctx->params.count_evals != 0 || evmap;
     if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 3 * sizeof(unsigned long long), ctx->stream));
@@ -464,6 +513,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
             : rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    if (pb) RM_HIP(hipEventRecord(pb->last, ctx->stream));
     if (sc && F.tile_cost) {  // sort this launch's durations on the side stream, overlapping the next launch
         const size_t slot = (sc->k / (uint64_t)sched_period()) & 1;
         uint32_t *h = sc->buf + 4 * (size_t)sc->n;
@@ -477,20 +527,32 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     }
     if (sc) {
         RM_HIP(hipEventRecord(sc->last, ctx->stream));
-        sc->k++;
+        if (!cnt) sc->k++;
     }
+    rm_status ms_st = mark_done(ctx);
+    if (ms_st != RM_OK) return ms_st;
     if (stats) {
         RM_HIP(hipEventSynchronize(ctx->ev1));
         float ms = 0.0f;
         RM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
         unsigned long long ev[3] = {0, 0, 0};
         if (cnt) RM_HIP(hipMemcpy(ev, ctx->d_evals, sizeof(ev), hipMemcpyDeviceToHost));
+        std::memset(stats, 0, sizeof(*stats));
         stats->evals = ev[0];
         stats->flop = ev[1];
         stats->skipped = ev[2];
         stats->pixels = (uint64_t)W * (uint64_t)count;
         stats->kernel_ms = ms;
         stats->scene = ctx->scene;
+        stats->dispatch = !F.tile_order ? RM_DISPATCH_ROW_MAJOR
+                          : F.tile_order == ctx->tile_order ? RM_DISPATCH_EXPLICIT
+                                                            : RM_DISPATCH_ADAPTIVE;
+        // the latency tiles: scene T, an ordered launch of one-wave tiles
+        // (rm_render_direct.h render_tile_at)
+        if (F.tile_order && ctx->scene == rm::SCENE_T && pick_kernel(ctx) != rm::KERNEL_TILE16) {
+            const rm::TileGrid g = rm::tile_grid(pick_kernel(ctx), W, count);
+            stats->lat_tiles = std::min(F.lat_tiles, g.x * g.y);
+        }
     }
     return RM_OK;
 }
@@ -510,7 +572,10 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     if (row_begin < 0 || row_count < 0 || row_begin + row_count > n)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: packed row range outside the shard");
     if (row_count == 0) {  // e.g. more shards than bands: nothing to do
-        if (stats) *stats = rm_stats{0, 0, 0.0f, ctx->scene, 0, 0};
+        if (stats) {
+            std::memset(stats, 0, sizeof(*stats));
+            stats->scene = ctx->scene;
+        }
         return RM_OK;
     }
     if (!out) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: null output");
@@ -583,6 +648,7 @@ rm_status classify_scene_file(const std::string &file, int &sc, std::string &src
 }  // namespace
 
 int rm_internal_device(const rm_ctx *ctx) { return ctx->device; }
+rm_status rm_internal_mark_done(rm_ctx *ctx) { return mark_done(ctx); }
 hipStream_t rm_internal_stream(const rm_ctx *ctx) { return ctx->stream; }
 int rm_internal_scene(const rm_ctx *ctx) { return ctx->scene; }
 void rm_internal_set_error(rm_ctx *ctx, const std::string &msg) { ctx->err = msg; }
@@ -603,6 +669,8 @@ rm_status rm_create(rm_ctx **out, int device) {
     if (e == hipSuccess) e = hipMalloc(&ctx->d_evals, 3 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming);
+    ctx->persist.reserve(rm_ctx::kPersistBlocks);
     if (e != hipSuccess) {
         rm_destroy(ctx);
         return e == hipErrorOutOfMemory ? RM_ERR_OUT_OF_MEMORY : RM_ERR_DEVICE;
@@ -614,12 +682,25 @@ rm_status rm_create(rm_ctx **out, int device) {
 rm_status rm_destroy(rm_ctx *ctx) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(ctx->device);
-    // nothing of this context still runs (its stream may be the caller's and
-    // already destroyed, so the device is synchronized instead)
-    (void)hipDeviceSynchronize();
+    // nothing this context enqueued still runs: its own events (the streams
+    // may be the caller's and gone by now) and its side stream; other work on
+    // the device is not waited for
+    if (ctx->done && ctx->done_recorded) (void)hipEventSynchronize(ctx->done);
+    for (hipEvent_t ev : ctx->retired) {
+        (void)hipEventSynchronize(ev);
+        (void)hipEventDestroy(ev);
+    }
+    for (auto &b : ctx->persist)
+        if (b.last) (void)hipEventSynchronize(b.last);
+    for (rm_ctx::Sched &e : ctx->sched)
+        if (e.last) (void)hipEventSynchronize(e.last);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
-    for (auto &sp : ctx->persist) (void)hipFree(sp.second);
+    for (auto &b : ctx->persist) {
+        if (b.ctr) (void)hipFree(b.ctr);
+        if (b.last) (void)hipEventDestroy(b.last);
+    }
     if (ctx->staging) (void)hipFree(ctx->staging);
     if (ctx->mips) (void)hipFree(ctx->mips);
     if (ctx->tile_order) (void)hipFree(ctx->tile_order);
@@ -627,6 +708,7 @@ rm_status rm_destroy(rm_ctx *ctx) {
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->done) (void)hipEventDestroy(ctx->done);
     delete ctx;
     return RM_OK;
 }
@@ -725,7 +807,25 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *p) {
 
 rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
-    ctx->stream = reinterpret_cast<hipStream_t>(stream);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (s != ctx->stream && ctx->done_recorded) {
+        // keep the old stream's last-work event until it completes; reuse a
+        // completed one for the new stream (no host wait here)
+        RM_HIP(hipSetDevice(ctx->device));
+        hipEvent_t next = nullptr;
+        for (size_t i = 0; i < ctx->retired.size(); i++)
+            if (hipEventQuery(ctx->retired[i]) == hipSuccess) {
+                next = ctx->retired[i];
+                ctx->retired.erase(ctx->retired.begin() + (long)i);
+                break;
+            }
+        (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+        if (!next) RM_HIP(hipEventCreateWithFlags(&next, hipEventDisableTiming));
+        ctx->retired.push_back(ctx->done);
+        ctx->done = next;
+        ctx->done_recorded = false;
+    }
+    ctx->stream = s;
     return RM_OK;
 }
 
@@ -834,7 +934,7 @@ static rm_status deinterleave_any(rm_ctx *ctx, int W, int H, int band, int nshar
                                                    reinterpret_cast<float4 *>(out), W, H, band, nshards,
                                                    rows_per_shard, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "deinterleave launch");
-    return RM_OK;
+    return mark_done(ctx);
 }
 
 rm_status rm_deinterleave(rm_ctx *ctx, int W, int H, int band, int nshards, int rows_per_shard, const float *gathered,
@@ -861,7 +961,7 @@ rm_status rm_pack_rgb8(rm_ctx *ctx, int64_t npixels, const uint32_t *in, uint8_t
     RM_HIP(hipSetDevice(ctx->device));
     hipError_t e = rm::launch_pack_rgb8(in, out, (size_t)npixels, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "pack_rgb8 launch");
-    return RM_OK;
+    return mark_done(ctx);
 }
 
 rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t *out) {
@@ -872,7 +972,7 @@ rm_status rm_pack_rgba8(rm_ctx *ctx, int64_t npixels, const float *in, uint32_t 
     RM_HIP(hipSetDevice(ctx->device));
     hipError_t e = rm::launch_pack_rgba8(reinterpret_cast<const float4 *>(in), out, (size_t)npixels, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "pack launch");
-    return RM_OK;
+    return mark_done(ctx);
 }
 
 rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) {
@@ -886,7 +986,7 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) 
     rm::TraceRange range("rm_fxaa");
     hipError_t e = rm::launch_fxaa(in, out, W, H, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "fxaa launch");
-    return RM_OK;
+    return mark_done(ctx);
 }
 
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) {
@@ -907,7 +1007,7 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
     }
     hipError_t e = rm::launch_bloom(in, out, ctx->mips, plan, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "bloom launch");
-    return RM_OK;
+    return mark_done(ctx);
 }
 
 rm_status rm_scene_eval(rm_ctx *ctx, const float *points, int64_t n, float *dist, float *material) {
@@ -961,6 +1061,8 @@ rm_status rm_compile_scene(const char *file_name, char *log, size_t log_size) {
     }
     return st;
 }
+
+int rm_abi_version(void) { return RM_ABI_VERSION; }
 
 const char *rm_last_error(rm_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 

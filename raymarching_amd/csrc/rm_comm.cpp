@@ -89,7 +89,8 @@ struct rm_comm {
     uint8_t *wire = nullptr;     // the same rows, RGB8 (rows_per_shard * 3W bytes)
     uint8_t *gathered = nullptr; // root: nranks wires
     size_t band_bytes = 0, wire_bytes = 0, gathered_bytes = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // render start / render end / gather end / de-interleave end (rm_stats)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     int rows_mine = 0, rows_per_shard = 0;
 };
 
@@ -129,6 +130,8 @@ rm_status comm_new(rm_comm **out, rm_ctx *ctx, int nranks, int rank) {
     hipError_t e = hipSetDevice(rm_internal_device(ctx));
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev2);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev3);
     if (e != hipSuccess) {
         rm_comm_destroy(c);
         return RM_ERR_DEVICE;
@@ -161,8 +164,18 @@ rm_status enqueue_local(rm_comm *c, int W, int H, int band) {
     return rm_pack_rgb8(ctx, (int64_t)n * W, c->band, c->wire);
 }
 
-// the gather of every rank's wire into rank 0's gathered buffer
+rm_status enqueue_gather_ops(rm_comm *c, int W);
+
+// the gather of every rank's wire into rank 0's gathered buffer, then ev2
 rm_status enqueue_gather(rm_comm *c, int W) {
+    rm_status st = enqueue_gather_ops(c, W);
+    if (st != RM_OK) return st;
+    if (hipEventRecord(c->ev2, rm_internal_stream(c->ctx)) != hipSuccess)
+        return comm_fail(c, RM_ERR_DEVICE, "hipEventRecord");
+    return rm_internal_mark_done(c->ctx);
+}
+
+rm_status enqueue_gather_ops(rm_comm *c, int W) {
     if (!c->nc) return RM_OK;  // a one-rank communicator without RCCL: the wire is the gathered buffer
     rm::TraceRange range("rm_gather");
     Rccl *R = rccl();
@@ -194,14 +207,21 @@ rm_status finish(rm_comm *c, int W, int H, int band, uint32_t *frame, rm_stats *
     if (c->rank == 0)
         st = rm_deinterleave_rgb8(c->ctx, W, H, band, c->nranks, c->rows_per_shard,
                                   c->nc ? c->gathered : c->wire, frame);
-    if (st != RM_OK || !stats) return st;
+    if (st != RM_OK) return st;
+    if (c->rank == 0 && hipEventRecord(c->ev3, rm_internal_stream(c->ctx)) != hipSuccess)
+        return comm_fail(c, RM_ERR_DEVICE, "hipEventRecord");
+    if (!stats) return RM_OK;
     if (hipStreamSynchronize(rm_internal_stream(c->ctx)) != hipSuccess)
         return comm_fail(c, RM_ERR_DEVICE, "hipStreamSynchronize");
-    float ms = 0.0f;
+    float ms = 0.0f, gms = 0.0f, dms = 0.0f;
     (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    (void)hipEventElapsedTime(&gms, c->ev1, c->ev2);
+    if (c->rank == 0) (void)hipEventElapsedTime(&dms, c->ev2, c->ev3);
     std::memset(stats, 0, sizeof(*stats));
     stats->pixels = (uint64_t)W * (uint64_t)c->rows_mine;
     stats->kernel_ms = ms;
+    stats->gather_ms = gms;
+    stats->deinterleave_ms = dms;
     stats->scene = rm_internal_scene(c->ctx);
     return RM_OK;
 }
@@ -315,6 +335,8 @@ rm_status rm_comm_destroy(rm_comm *c) {
     if (c->gathered) (void)hipFree(c->gathered);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
+    if (c->ev3) (void)hipEventDestroy(c->ev3);
     delete c;
     return RM_OK;
 }
@@ -356,11 +378,19 @@ rm_status rm_render_sharded_all(rm_comm *const *comms, int n, int W, int H, int 
         rm_status st = nccl_check(comms[0], R->GroupStart(), "ncclGroupStart");
         for (int i = 0; i < n && st == RM_OK; i++) {
             (void)hipSetDevice(rm_internal_device(comms[i]->ctx));
-            st = enqueue_gather(comms[i], W);
+            st = enqueue_gather_ops(comms[i], W);
         }
         rm_status st2 = nccl_check(comms[0], R->GroupEnd(), "ncclGroupEnd");
         if (st != RM_OK) return st;
         if (st2 != RM_OK) return st2;
+        // the grouped gathers reach the streams at ncclGroupEnd: their end events after it
+        for (int i = 0; i < n; i++) {
+            (void)hipSetDevice(rm_internal_device(comms[i]->ctx));
+            if (hipEventRecord(comms[i]->ev2, rm_internal_stream(comms[i]->ctx)) != hipSuccess)
+                return comm_fail(comms[i], RM_ERR_DEVICE, "hipEventRecord");
+            st = rm_internal_mark_done(comms[i]->ctx);
+            if (st != RM_OK) return st;
+        }
     }
     (void)hipSetDevice(rm_internal_device(comms[0]->ctx));
     for (int i = 0; i < n; i++) {

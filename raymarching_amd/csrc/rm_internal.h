@@ -10,4 +10,6 @@
 int rm_internal_device(const rm_ctx *ctx);
 hipStream_t rm_internal_stream(const rm_ctx *ctx);
 int rm_internal_scene(const rm_ctx *ctx);
+// record that work was enqueued on the ctx stream (rm_destroy waits for it)
+rm_status rm_internal_mark_done(rm_ctx *ctx);
 void rm_internal_set_error(rm_ctx *ctx, const std::string &msg);

@@ -251,3 +251,60 @@ class DistributedFrame:
         """One complete frame (submit + flush)."""
         self.submit(events)
         return self.flush()
+
+    def timed_exchange(self):
+        """One frame with its steps run one after another and each timed alone
+        (nothing pipelined): this rank's render, the RGB8 pack, then -- once
+        every rank has packed (barrier) -- the gather, and on rank 0 the
+        de-interleave.  Collective (every rank calls it).  Returns ms per step:
+        render_ms, pack_ms, gather_ms (the transfer alone: HIP events around the
+        RCCL gather on the frame stream; with gloo, wall time of the host-staged
+        gather), deinterleave_ms (rank 0, else 0).  The frame lands in slot 0."""
+        import time
+
+        import torch
+        import torch.distributed as dist
+
+        p, st, slot = self.plan, self.streams[0], 0
+        dev = torch.device(f"cuda:{self.r.device}")
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        self.flush()
+        torch.cuda.synchronize(dev)
+        self.r.set_stream(st)
+        with torch.cuda.stream(st):
+            ev[0].record(st)
+            if self.nmine:
+                dst = self.wires[slot] if self.locals is None else self.locals[slot]
+                self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, 0, self.nmine, dst[: self.nmine])
+            ev[1].record(st)
+            if self.locals is not None and self.nmine:
+                self.r.pack_rgb8(self.locals[slot][: self.nmine], out=self.wires[slot][: self.nmine])
+            ev[2].record(st)
+        torch.cuda.synchronize(dev)
+        out = dict(render_ms=ev[0].elapsed_time(ev[1]), pack_ms=ev[1].elapsed_time(ev[2]), gather_ms=0.0,
+                   deinterleave_ms=0.0)
+        if self.world == 1:
+            return out
+        dist.barrier(group=self.group)
+        if self._pipelined():
+            with torch.cuda.stream(st):
+                ev[3].record(st)
+                self._gather_async(slot, 0, p.rows_per_shard).wait()  # st waits for the gather
+                ev[4].record(st)
+            torch.cuda.synchronize(dev)
+            out["gather_ms"] = ev[3].elapsed_time(ev[4])
+        else:  # gloo: host-staged, completes inside the call
+            t0 = time.perf_counter()
+            gather_to_root(self.wires[slot], p, self.rank, group=self.group,
+                           out=self.gathered[slot] if self.rank == 0 else None)
+            torch.cuda.synchronize(dev)
+            out["gather_ms"] = (time.perf_counter() - t0) * 1e3
+        if self.rank == 0:
+            with torch.cuda.stream(st):
+                ev[4].record(st)
+                self._deinterleave(slot)
+                ev[5].record(st)
+            torch.cuda.synchronize(dev)
+            out["deinterleave_ms"] = ev[4].elapsed_time(ev[5])
+            self.frame = self.frames[slot]
+        return out

@@ -105,10 +105,10 @@ int run_all(int n) {
     if (hipMalloc(&frame, (size_t)g_W * g_H * 4) != hipSuccess) return 1;
     bool equal = true;
     int frames = 0;
+    std::vector<rm_stats> st(n);
     for (int f = 0; f < 2; f++) {
         for (int i = 0; i < n; i++)
             if (!setup(ctx[i], kPoses[f])) return 1;
-        std::vector<rm_stats> st(n);
         if (rm_render_sharded_all(comm.data(), n, g_W, g_H, g_band, frame, st.data()) != RM_OK) {
             std::fprintf(stderr, "rm_render_sharded_all: %s\n", rm_last_error(ctx[0]));
             return 1;
@@ -123,8 +123,10 @@ int run_all(int n) {
         frames++;
     }
     std::printf("{\"mode\": \"all\", \"n\": %d, \"W\": %d, \"H\": %d, \"band\": %d, \"frames\": %d, \"equal\": %s, "
-                "\"uses_rccl\": %d, \"standin_stats\": %s}\n",
-                n, g_W, g_H, g_band, frames, equal ? "true" : "false", uses, standin_stats().c_str());
+                "\"uses_rccl\": %d, \"standin_stats\": %s, \"root_ms\": [%g, %g, %g], \"last_rank_ms\": [%g, %g, %g]}\n",
+                n, g_W, g_H, g_band, frames, equal ? "true" : "false", uses, standin_stats().c_str(), st[0].kernel_ms,
+                st[0].gather_ms, st[0].deinterleave_ms, st[n - 1].kernel_ms, st[n - 1].gather_ms,
+                st[n - 1].deinterleave_ms);
     for (rm_comm *c : comm) rm_comm_destroy(c);
     (void)hipFree(frame);
     for (rm_ctx *c : ctx) rm_destroy(c);
@@ -138,6 +140,7 @@ struct Shared {  // MAP_SHARED | MAP_ANONYMOUS, created before the fork
     std::atomic<int> frames;
     std::atomic<int> uses_rccl;
     char stats[128];
+    float root_ms[3];  // rank 0's rm_stats of the last frame: kernel, gather, de-interleave
 };
 
 int rank_worker(Shared *sh, int n, int rank) {
@@ -166,9 +169,10 @@ int rank_worker(Shared *sh, int n, int rank) {
     }
     uint32_t *frame = nullptr;
     if (rank == 0 && hipMalloc(&frame, (size_t)g_W * g_H * 4) != hipSuccess) return 1;
+    rm_stats st{};
     for (int f = 0; f < 2; f++) {
         if (!setup(ctx, kPoses[f])) return 1;
-        if (rm_render_sharded(comm, g_W, g_H, g_band, frame, nullptr) != RM_OK) {
+        if (rm_render_sharded(comm, g_W, g_H, g_band, frame, rank == 0 ? &st : nullptr) != RM_OK) {
             std::fprintf(stderr, "rank %d rm_render_sharded: %s\n", rank, rm_last_error(ctx));
             return 1;
         }
@@ -187,6 +191,9 @@ int rank_worker(Shared *sh, int n, int rank) {
         rm_comm_info(comm, nullptr, nullptr, &uses);
         sh->uses_rccl.store(uses);
         std::snprintf(sh->stats, sizeof(sh->stats), "%s", standin_stats().c_str());
+        sh->root_ms[0] = st.kernel_ms;
+        sh->root_ms[1] = st.gather_ms;
+        sh->root_ms[2] = st.deinterleave_ms;
     }
     rm_comm_destroy(comm);
     if (frame) (void)hipFree(frame);
@@ -217,9 +224,9 @@ int run_ranks(int n) {
     }
     const bool equal = !bad && sh->equal.load() == 1 && sh->frames.load() == 2;
     std::printf("{\"mode\": \"ranks\", \"n\": %d, \"W\": %d, \"H\": %d, \"band\": %d, \"frames\": %d, \"equal\": %s, "
-                "\"failed_ranks\": %d, \"uses_rccl\": %d, \"standin_stats\": %s}\n",
+                "\"failed_ranks\": %d, \"uses_rccl\": %d, \"standin_stats\": %s, \"root_ms\": [%g, %g, %g]}\n",
                 n, g_W, g_H, g_band, sh->frames.load(), equal ? "true" : "false", bad, sh->uses_rccl.load(),
-                sh->stats[0] ? sh->stats : "null");
+                sh->stats[0] ? sh->stats : "null", sh->root_ms[0], sh->root_ms[1], sh->root_ms[2]);
     return equal ? 0 : 3;
 }
 

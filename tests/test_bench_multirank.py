@@ -1,0 +1,64 @@
+"""bench.py end to end, small: the frame check (the timed kernel's last frame
+equals the instrumented kernel's, bit for bit) and, for N > 1 ranks, the
+exchange figures the scaling run reports (gather_ms, deinterleave_ms,
+kernel_ms per rank).  N = 2 with the gloo backend is the one-GPU rehearsal of
+the multi-rank path (two ranks on device 0, host-staged gather); the RCCL
+("nccl") run needs two GPUs and is skipped below that."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--steps", "3", "--warmup", "1", "--spinup", "0", "--size", "512", "--cpu-seconds", "0"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd):
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-3000:])
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _torchrun(n, extra):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(n)] + extra
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["T", "O"])
+def test_bench_one_gpu_frame_check(torch_cuda, scene):
+    res = _run([sys.executable, "bench.py"] + SMALL + ["--scene", scene])
+    assert res["frame_check"]["result"] == "bit-exact" and res["frame_check"]["pixels"] == 512 * 512, res
+    assert res["n_gpus"] == 1 and "gather_ms" not in res
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_rehearsal(torch_cuda):
+    """Two ranks on one GPU over gloo: the whole multi-rank path of bench.py
+    (row bands, RGB8 wire, gather, de-interleave) and its exchange figures."""
+    res = _run(_torchrun(2, SMALL + ["--backend", "gloo"]))
+    assert res["n_gpus"] == 2 and res["frame_check"]["result"] == "bit-exact", res
+    assert len(res["kernel_ms_per_rank"]) == 2 and all(k > 0 for k in res["kernel_ms_per_rank"]), res
+    assert res["gather_ms"] > 0 and res["deinterleave_ms"] > 0 and res["backend"] == "gloo", res
+    assert res["root_ingress_bytes"] == res["wire_bytes_per_rank"] == 256 * 3 * 512, res
+
+
+@pytest.mark.gpu
+def test_bench_two_gpus_rccl(torch_cuda):
+    """The same over RCCL, one rank per GPU (skipped below two GPUs)."""
+    if torch_cuda.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
+    res = _run(_torchrun(2, SMALL))
+    assert res["n_gpus"] == 2 and res["frame_check"]["result"] == "bit-exact", res
+    assert res["gather_ms"] > 0 and res["deinterleave_ms"] > 0 and res["backend"] == "nccl", res

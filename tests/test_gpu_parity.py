@@ -402,7 +402,47 @@ def full_size_parity(r, scene, W, H, pose, steps, rows, col_block=None):
     exact = match / n
     print(f"{scene} {W}x{H} {steps} steps: {n} px, {stats}, step map exact {exact:.5f}")
     assert exact >= STEP_MAP_EXACT, exact
+    timed_path_equals_instrumented(r, scene, W, H, img)
     return n, stats, exact
+
+
+def timed_path_equals_instrumented(r, scene, W, H, img, launches=10):
+    """The kernels bench.py times (count_evals=0: the settled-shadow,
+    back-face and depth-3 reflection exits) against the
+    instrumented frame `img` (every reference ray-step; the frame the oracle
+    checks), bit for bit over the whole frame: float4 row-major
+    (schedule=0), then RGBA8 as bench renders it -- adaptive order
+    after `launches` launches, so a sorted order and, in scene T, the latency
+    tiles (2.8) are in effect -- and float4 in that order.  NaN pixels (OG)
+    compare by their bits.  References: common.frag:810-831 (soft shadow),
+    :931-954 and :991-1002 (castRay in getColorReflect); template.frag:45-76."""
+    torch = pytest.importorskip("torch")
+    r.set_params(count_evals=0, schedule=0)
+    ref_bits = img.view(torch.int32)
+    f, st = r.render(W, H, stats=True)
+    assert st["dispatch"] == "row-major", st
+    assert torch.equal(f.view(torch.int32), ref_bits), f"{scene} {W}x{H}: timed float4 (row-major) != instrumented"
+    del f
+    r.set_params(schedule=1)
+    ref8 = r.pack_rgba8(img)
+    out8 = torch.empty((H, W), dtype=torch.int32, device=img.device)
+    for _ in range(launches):
+        r.render_rgba8(W, H, out=out8)
+    _, st8 = r.render_rgba8(W, H, out=out8, stats=True)
+    assert st8["dispatch"] == "adaptive", st8
+    ntiles = ((W + 7) // 8) * ((H + 7) // 8)
+    if scene == "T":
+        assert st8["lat_tiles"] == min(2048, ntiles), st8
+    else:
+        assert st8["lat_tiles"] == 0, st8
+    n8 = int((out8 != ref8).sum())
+    assert n8 == 0, f"{scene} {W}x{H}: {n8} RGBA8 pixels of the timed, ordered frame differ from the instrumented frame"
+    f, st = r.render(W, H, stats=True)
+    assert st["dispatch"] == "adaptive", st
+    assert torch.equal(f.view(torch.int32), ref_bits), f"{scene} {W}x{H}: timed float4 (ordered) != instrumented"
+    print(f"{scene} {W}x{H}: timed kernel == instrumented frame (float4 row-major and ordered, RGBA8 ordered with "
+          f"{st8['lat_tiles']} latency tiles), {st8['kernel_ms']:.3f} ms")
+    r.set_params(count_evals=1)
 
 
 def test_c2_1080p_poses(R, torch_cuda):

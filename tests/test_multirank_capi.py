@@ -74,6 +74,10 @@ def test_render_sharded_all_n_contexts(torch_cuda, variant, n, W, H, band, scene
     group of n gathers (or n - 1 send/recv pairs) runs through the stand-in."""
     res = run_driver("all", n, W, H, band, scene, standin=variant)
     assert res["equal"] and res["frames"] == 2 and res["uses_rccl"] == 1, res
+    # rm_stats of a sharded frame: render, pack + gather, and on rank 0 the de-interleave
+    k, g, d = res["root_ms"]
+    assert k > 0 and g > 0 and d > 0, res
+    assert res["last_rank_ms"][0] > 0 and res["last_rank_ms"][2] == 0, res
     g, s, r, groups = res["standin_stats"]
     if variant == "gather":
         assert g == 2 and s == r == 0, res
@@ -92,6 +96,8 @@ def test_render_sharded_n_processes(torch_cuda, variant, n, W, H, band, scene):
     memory."""
     res = run_driver("ranks", n, W, H, band, scene, standin=variant)
     assert res["equal"] and res["frames"] == 2 and res["failed_ranks"] == 0 and res["uses_rccl"] == 1, res
+    k, g, d = res["root_ms"]
+    assert k > 0 and g > 0 and d > 0, res
     g, s, r, _ = res["standin_stats"]  # rank 0's process
     assert (g, r) == ((2, 0) if variant == "gather" else (0, 2 * (n - 1))), res
 
