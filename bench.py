@@ -172,7 +172,7 @@ def frame_check(r, frame, W, H, fmt):
     so the two frames must be the same bits; anything else fails the run."""
     import torch
 
-    timed = frame.clone()
+    timed = frame
     r.set_params(count_evals=1)
     ref = r.render_rgba8(W, H) if fmt == "rgba8" else r.render(W, H)
     r.set_params(count_evals=0)
@@ -413,8 +413,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-    # the last timed frame against the instrumented kernel's frame of the same pose (rank 0)
-    check = frame_check(r, fr.frame, W, H, args.fmt) if rank == 0 else None
+    last_frame = fr.frame.clone() if fr.frame is not None else None  # the last timed frame (rank 0)
     live = [c for c in range(nch) if min(fr.cuts[c + 1], fr.nmine) > fr.cuts[c]]  # chunks with rows here
     # per-frame interval of the render calls on the frame stream (events around each call: the render
     # kernel plus the dispatch-order sort it enqueues; with 2 streams it also spans overlapping frames)
@@ -429,6 +428,8 @@ def main():
     launch = sorted(fr.render_local(stats=True)[1]["kernel_ms"] for _ in range(11)) if fr.nmine else [0.0]
     kern = launch[len(launch) // 2]
     kt = torch.tensor([kern], dtype=torch.float64, device=red_dev)
+    # the last timed frame against the instrumented kernel's frame of the same pose (rank 0)
+    check = frame_check(r, last_frame, W, H, args.fmt) if rank == 0 else None
     exchange = None
     if world > 1:
         # the frame's steps one at a time (render, pack, gather, de-interleave),

@@ -341,8 +341,13 @@ __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& 
 #endif
 }
 
+// (the probe form's sum of squares fused: RM_PROBE_FMA_O, rm_render_direct.h)
+#ifndef RM_PROBE_FMA_O
+#define RM_PROBE_FMA_O 1
+#endif
 template <bool EXACT>
 __device__ __forceinline__ float len3(float x, float y, float z) {
+    if constexpr (!EXACT && RM_PROBE_FMA_O) return __builtin_amdgcn_sqrtf(fmaf(z, z, fmaf(y, y, x * x)));
     float l2 = x * x + y * y + z * z;
     return EXACT ? sqrtf(l2) : __builtin_amdgcn_sqrtf(l2);
 }

@@ -224,8 +224,9 @@ bool compile(const std::string& src, const std::string& file, Code& code, std::s
     const char* env_w = std::getenv("RM_PLUGIN_WAVES_PER_EU");
     const std::string waves = std::string("-DRM_PLUGIN_WAVES_PER_EU=") +
                               (env_w && std::atoi(env_w) > 0 ? std::to_string(std::atoi(env_w)) : std::string("1"));
+    // (no SLP vectorization, as librm's own device code: raymarching_amd/Makefile DEVFLAGS)
     const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                          "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wno-unused-function",
+                          "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", "-Wno-unused-function",
                           "-Wno-unused-variable", waves.c_str()};
     r = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
     size_t ls = 0;

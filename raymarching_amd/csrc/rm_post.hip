@@ -111,8 +111,106 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
     }
 }
 
+// The LDS-staged form (the default).  A workgroup renders a 64x32-pixel tile
+// from the texels it can reach, staged once in LDS with their luma:
+//  * the five +-1 / centre taps land on integer texels.  With fx = (x+.5)/W and
+//    ivx = 1/W correctly rounded, (fx - ivx) W = x - 0.5 up to three
+//    roundings of relative size 2^-24, i.e. within 3 * 2^-24 * (x + 1.5) <
+//    0.5 for W <= 2^20, so floor gives x - 1 (x, x + 1 likewise; rows: 1 -
+//    (y+.5)/H flips to H - 1 - y, +-1).  Their texel and luma are LDS reads:
+//    no float address math, and each texel's luma is formed once per tile
+//    instead of once per tap (same operations, same order: the same bits);
+//  * the four span taps keep post.frag's float addressing exactly (fx + dx k,
+//    NEAREST, CLAMP_TO_EDGE); dx, dy are clamped to +-8 texels and k <= 0.5,
+//    so they stay within 4 texels (+ rounding) of the pixel: a halo of 5
+//    covers them, and a tap outside the staged block (not reachable, kept for
+//    safety) reads global memory.
+// Frames wider or taller than 2^20 use rm_fxaa_kernel.
+#ifndef RM_FXAA_TY
+#define RM_FXAA_TY 32
+#endif
+constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
+constexpr int FXL_MAX_DIM = 1 << 20;
+__global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                          int W, int H) {
+    __shared__ uint32_t stex[FXL_H * FXL_W];
+    __shared__ float slum[FXL_H * FXL_W];
+    const int x0 = blockIdx.x * FXL_TX, y0 = blockIdx.y * FXL_TY;
+    // output rows y0 .. y0 + TY - 1 read texel rows H-1-y (+-1, span): the block
+    // [tx0, tx0 + FXL_W) x [ty0, ty0 + FXL_H), each texel clamped to the frame
+    const int tx0 = x0 - FXL_HALO, ty0 = H - (y0 + FXL_TY) - FXL_HALO;
+    // every load of the block in flight before the first LDS store
+    constexpr int NIT = (FXL_W * FXL_H + 255) / 256;
+    uint32_t tv[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; k++) {
+        const int i = (int)threadIdx.x + 256 * k;
+        const int r = i / FXL_W, c = i - r * FXL_W;
+        const int gx = clamp_med3(tx0 + c, W - 1), gy = clamp_med3(ty0 + (r < FXL_H ? r : FXL_H - 1), H - 1);
+        tv[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(in) + (uint32_t)(gy * W + gx) * 4u);
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; k++) {
+        const int i = (int)threadIdx.x + 256 * k;
+        if (i < FXL_W * FXL_H) {
+            stex[i] = tv[k];
+            slum[i] = luma(rgb(tv[k]));
+        }
+    }
+    __syncthreads();
+    const float FXAA_REDUCE_MIN = 1.0f / 128.0f, FXAA_REDUCE_MUL = 1.0f / 8.0f, FXAA_SPAN_MAX = 8.0f;
+    const float ivx = 1.0f / (float)W, ivy = 1.0f / (float)H;  // inverseVP = 1 / u_resolution
+    const float k1 = 1.0f / 3.0f - 0.5f, k2 = 2.0f / 3.0f - 0.5f;
+    const int lx = threadIdx.x & 63, x = x0 + lx;
+    // a span tap: post.frag's float address, then the staged texel
+    auto span_tap = [&](float u, float v) -> RGB {
+        const int gx = clamp_med3((int)floorf(u * (float)W), W - 1) - tx0;
+        const int gy = clamp_med3((int)floorf(v * (float)H), H - 1) - ty0;
+        if ((unsigned)gx < (unsigned)FXL_W && (unsigned)gy < (unsigned)FXL_H) return rgb(stex[gy * FXL_W + gx]);
+        return rgb(texel(in, W, H, u, v));
+    };
+    for (int ly = threadIdx.x >> 6; ly < FXL_TY; ly += 4) {
+        const int y = y0 + ly;
+        if (x >= W || y >= H) continue;
+        // centre texel (x, H-1-y) in the block
+        const int m = (FXL_TY - 1 - ly + FXL_HALO) * FXL_W + (lx + FXL_HALO);
+        const float lNW = slum[m - FXL_W - 1], lNE = slum[m - FXL_W + 1], lSW = slum[m + FXL_W - 1];
+        const float lSE = slum[m + FXL_W + 1], lM = slum[m];
+        const uint32_t tM = stex[m];
+        const float fx = ((float)x + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
+        const float fy = 1.0f - ((float)y + 0.5f) / (float)H;
+        float lMin = gmin_(lM, gmin_(gmin_(lNW, lNE), gmin_(lSW, lSE)));
+        float lMax = gmax_(lM, gmax_(gmax_(lNW, lNE), gmax_(lSW, lSE)));
+        float dx = -((lNW + lNE) - (lSW + lSE));
+        float dy = ((lNW + lSW) - (lNE + lSE));
+        float dirReduce = gmax_((lNW + lNE + lSW + lSE) * (0.25f * FXAA_REDUCE_MUL), FXAA_REDUCE_MIN);
+        float rcpDirMin = 1.0f / (gmin_(fabsf(dx), fabsf(dy)) + dirReduce);
+        dx = gmin_(FXAA_SPAN_MAX, gmax_(-FXAA_SPAN_MAX, dx * rcpDirMin)) * ivx;
+        dy = gmin_(FXAA_SPAN_MAX, gmax_(-FXAA_SPAN_MAX, dy * rcpDirMin)) * ivy;
+        RGB s1 = span_tap(fx + dx * k1, fy + dy * k1);
+        RGB s2 = span_tap(fx + dx * k2, fy + dy * k2);
+        RGB a = RGB{(s1.r + s2.r) * 0.5f, (s1.g + s2.g) * 0.5f, (s1.b + s2.b) * 0.5f};
+        RGB s3 = span_tap(fx + dx * -0.5f, fy + dy * -0.5f);
+        RGB s4 = span_tap(fx + dx * 0.5f, fy + dy * 0.5f);
+        RGB b = RGB{a.r * 0.5f + (s3.r + s4.r) * 0.25f, a.g * 0.5f + (s3.g + s4.g) * 0.25f,
+                    a.b * 0.5f + (s3.b + s4.b) * 0.25f};
+        float lB = luma(b);
+        RGB c = (lB < lMin || lB > lMax) ? a : b;
+        float alpha = (float)(tM >> 24) * (1.0f / 255.0f);
+        out[(size_t)y * W + x] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | (unorm8(alpha) << 24);
+    }
+}
+
+#ifndef RM_FXAA_LDS
+#define RM_FXAA_LDS 1
+#endif
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s) {
     if (W <= 0 || H <= 0) return hipSuccess;
+    if (RM_FXAA_LDS && W <= FXL_MAX_DIM && H <= FXL_MAX_DIM) {
+        dim3 grid((W + FXL_TX - 1) / FXL_TX, (H + FXL_TY - 1) / FXL_TY);
+        hipLaunchKernelGGL(rm_fxaa_lds_kernel, grid, dim3(256), 0, s, in, out, W, H);
+        return hipGetLastError();
+    }
     dim3 grid((W + FXAA_TX - 1) / FXAA_TX, (H + FXAA_TY - 1) / FXAA_TY);
     hipLaunchKernelGGL(rm_fxaa_kernel, grid, dim3(256), 0, s, in, out, W, H);
     return hipGetLastError();
