@@ -259,9 +259,10 @@ hipError_t load(const Code& code, Module& m) {
     Module n;
     hipError_t e = hipModuleLoadData(&n.mod, code->data());
     if (e != hipSuccess) return e;
-    if (hipModuleGetFunction(&n.render, n.mod, "rm_plugin_render") != hipSuccess) {
+    if (hipModuleGetFunction(&n.render, n.mod, "rm_plugin_render") != hipSuccess ||
+        hipModuleGetFunction(&n.render_count, n.mod, "rm_plugin_render_count") != hipSuccess) {
         (void)hipGetLastError();
-        n.render = nullptr;
+        n.render = n.render_count = nullptr;
     }
     e = hipModuleGetFunction(&n.eval, n.mod, "rm_plugin_eval");
     if (e != hipSuccess) {
@@ -281,14 +282,14 @@ void unload(Module& m) {
 
 hipError_t launch_render(const Module& m, const rm::FrameConst& F, void* out, bool rgba8, unsigned long long* evals,
                          hipStream_t s) {
-    if (!m.render) return hipErrorInvalidDeviceFunction;
+    if (!m.render || !m.render_count) return hipErrorInvalidDeviceFunction;
     rm::FrameConst f = F;
     void* o = out;
     int r8 = rgba8 ? 1 : 0;
     unsigned long long* e = evals;
     void* args[] = {&f, &o, &r8, &e};
-    return hipModuleLaunchKernel(m.render, (unsigned)((F.W + 7) / 8), (unsigned)((F.nrows + 7) / 8), 1, 64, 1, 1, 0,
-                                 s, args, nullptr);
+    return hipModuleLaunchKernel(evals ? m.render_count : m.render, (unsigned)((F.W + 7) / 8),
+                                 (unsigned)((F.nrows + 7) / 8), 1, 64, 1, 1, 0, s, args, nullptr);
 }
 
 hipError_t launch_eval(const Module& m, const rm::FrameConst& F, const float* pts, long long n, float* dist,

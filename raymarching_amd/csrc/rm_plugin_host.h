@@ -28,7 +28,8 @@ bool compile(const std::string& src, const std::string& file, Code& code, std::s
 
 struct Module {
     hipModule_t mod = nullptr;
-    hipFunction_t render = nullptr;  // null for an RM_PLUGIN_EVAL_ONLY scene
+    hipFunction_t render = nullptr;        // timed render kernel; null for an RM_PLUGIN_EVAL_ONLY scene
+    hipFunction_t render_count = nullptr;  // instrumented render kernel (ray-step counts, step maps)
     hipFunction_t eval = nullptr;
     Code code;
 };

@@ -16,17 +16,20 @@ struct rm::PluginScene<rm::SCENE_PLUGIN> {
 };
 
 #ifndef RM_PLUGIN_EVAL_ONLY
-// output_shader.frag's pass over 8x8-pixel one-wave tiles.  One kernel serves
-// every launch: the output format and the instrumentation are run-time
-// arguments (a plugin compiles one pipeline instead of four).
+// output_shader.frag's pass over 8x8-pixel one-wave tiles, as two kernels: the
+// timed one (rm_plugin_render) and the instrumented one (rm_plugin_render_count:
+// ray-step tallies and step maps).  One kernel serving both paid the
+// instrumented pipeline's registers in every timed launch (occupancy 5).  The
+// output format is a run-time argument.
 // Minimum waves per SIMD for the register allocator (rm_plugin_host.cpp sets
-// it; a scene's pipeline needs ~150 VGPRs unbounded, occupancy 3).
+// it, default 1 = unconstrained).
 #ifndef RM_PLUGIN_WAVES_PER_EU
 #define RM_PLUGIN_WAVES_PER_EU 1
 #endif
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_PLUGIN_WAVES_PER_EU))) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
-                                                                  unsigned long long* evals) {
-    using namespace rm;
+namespace rm {
+template <bool COUNT>
+__device__ __forceinline__ void plugin_render_tile(const FrameConst& F, void* out, int rgba8,
+                                                   unsigned long long* evals) {
     const uint64_t t_start = F.tile_cost ? clock64() : 0;
     glsl::plugin_bind_uniforms(F);
     const int lane = threadIdx.x;
@@ -47,7 +50,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R
         // the exact skips of scene O's pipeline that hold for any scene (the soft
         // shadows of points facing away from the light): taken
         // by the timed launches, counted by the instrumented ones
-        V3 c = evals ? render_pixel<SCENE_PLUGIN, 3, 2>(F, ro, rd, cnt) : render_pixel<SCENE_PLUGIN, 3, 1>(F, ro, rd, cnt);
+        V3 c = render_pixel<SCENE_PLUGIN, 3, COUNT ? 2 : 1>(F, ro, rd, cnt);
         c = post_colour<false>(c, vig);
         const size_t i = (size_t)j * F.W + x;
         if (rgba8) store_pixel(F, static_cast<uint32_t*>(out), i, c);
@@ -57,7 +60,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R
         const uint64_t dt = clock64() - t_start;
         F.tile_cost[by * gridDim.x + bx] = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;
     }
-    if (evals) {
+    if constexpr (COUNT) {
         if (F.evals_map && x < F.W && j < F.nrows) F.evals_map[(size_t)j * F.W + x] = cnt.evals;
         uint32_t se = wave_sum_u32(cnt.evals), sf = wave_sum_u32(cnt.flop), ss = wave_sum_u32(cnt.skipped);
         if (lane == 0) {
@@ -66,6 +69,15 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(R
             if (ss) atomicAdd(&evals[2], (unsigned long long)ss);
         }
     }
+}
+}  // namespace rm
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_PLUGIN_WAVES_PER_EU))) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
+                                                                  unsigned long long* evals) {
+    rm::plugin_render_tile<false>(F, out, rgba8, evals);
+}
+extern "C" __global__ __launch_bounds__(64) void rm_plugin_render_count(rm::FrameConst F, void* out, int rgba8,
+                                                                         unsigned long long* evals) {
+    rm::plugin_render_tile<true>(F, out, rgba8, evals);
 }
 #endif
 

@@ -121,16 +121,34 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 //    no float address math, and each texel's luma is formed once per tile
 //    instead of once per tap (same operations, same order: the same bits);
 //  * the four span taps keep post.frag's float addressing exactly (fx + dx k,
-//    NEAREST, CLAMP_TO_EDGE); dx, dy are clamped to +-8 texels and k <= 0.5,
-//    so they stay within 4 texels (+ rounding) of the pixel: a halo of 5
-//    covers them, and a tap outside the staged block (not reachable, kept for
-//    safety) reads global memory.
+//    NEAREST).  dx, dy are clamped to +-8 texels and |k| <= 0.5, so u W lies
+//    within x + 0.5 +- 4 (+ roundings far below 0.5 for W <= 2^20) and the
+//    texel within x +- 4: inside the block (halo 5).  The block holds the
+//    CLAMP_TO_EDGE texel of every position, so the unclamped index minus the
+//    block origin addresses it (clamped into the block, which only guards
+//    memory: the bound above keeps it inside);
+//  * lumas of unorm8 texels are never NaN, so GLSL min/max are v_min3/v_max3
+//    and the span clamp one v_med3.
 // Frames wider or taller than 2^20 use rm_fxaa_kernel.
 #ifndef RM_FXAA_TY
 #define RM_FXAA_TY 32
 #endif
 constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
 constexpr int FXL_MAX_DIM = 1 << 20;
+__device__ __forceinline__ int clamp_to(int v, int hi) {  // v_med3_i32(v, 0, hi)
+    int r;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "v"(hi));
+    return r;
+}
+__device__ __forceinline__ int floor_i32(float v) {  // (int)floorf(v) for |v| < 2^31: one v_cvt_flr_i32_f32
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+// unorm8 of a finite colour: clamp as one v_med3, round to nearest
+__device__ __forceinline__ uint32_t unorm8_finite(float c) {
+    return (uint32_t)__float2int_rn(__builtin_amdgcn_fmed3f(c, 0.0f, 1.0f) * 255.0f);
+}
 __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                           int W, int H) {
     __shared__ uint32_t stex[FXL_H * FXL_W];
@@ -139,54 +157,62 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     // output rows y0 .. y0 + TY - 1 read texel rows H-1-y (+-1, span): the block
     // [tx0, tx0 + FXL_W) x [ty0, ty0 + FXL_H), each texel clamped to the frame
     const int tx0 = x0 - FXL_HALO, ty0 = H - (y0 + FXL_TY) - FXL_HALO;
-    // every load of the block in flight before the first LDS store
-    constexpr int NIT = (FXL_W * FXL_H + 255) / 256;
-    uint32_t tv[NIT];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // staging: wave wv loads block rows wv, wv + 4, ...; lane -> column lane and
+    // lane + 64 (the last FXL_W - 64 columns); every load in flight before the
+    // first LDS store
+    constexpr int NR = (FXL_H + 3) / 4;
+    const int gx0 = clamp_med3(tx0 + lane, W - 1), gx1 = clamp_med3(tx0 + 64 + (lane < FXL_W - 64 ? lane : 0), W - 1);
+    uint32_t t0[NR], t1[NR];
 #pragma unroll
-    for (int k = 0; k < NIT; k++) {
-        const int i = (int)threadIdx.x + 256 * k;
-        const int r = i / FXL_W, c = i - r * FXL_W;
-        const int gx = clamp_med3(tx0 + c, W - 1), gy = clamp_med3(ty0 + (r < FXL_H ? r : FXL_H - 1), H - 1);
-        tv[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(in) + (uint32_t)(gy * W + gx) * 4u);
+    for (int k = 0; k < NR; k++) {
+        const int r = wv + 4 * k;
+        const int gy = clamp_med3(ty0 + (r < FXL_H ? r : FXL_H - 1), H - 1);
+        const char* row = reinterpret_cast<const char*>(in) + (uint32_t)(gy * W) * 4u;
+        t0[k] = *reinterpret_cast<const uint32_t*>(row + (uint32_t)gx0 * 4u);
+        t1[k] = *reinterpret_cast<const uint32_t*>(row + (uint32_t)gx1 * 4u);
     }
 #pragma unroll
-    for (int k = 0; k < NIT; k++) {
-        const int i = (int)threadIdx.x + 256 * k;
-        if (i < FXL_W * FXL_H) {
-            stex[i] = tv[k];
-            slum[i] = luma(rgb(tv[k]));
+    for (int k = 0; k < NR; k++) {
+        const int r = wv + 4 * k;
+        if (r < FXL_H) {
+            stex[r * FXL_W + lane] = t0[k];
+            slum[r * FXL_W + lane] = luma(rgb(t0[k]));
+            if (lane < FXL_W - 64) {
+                stex[r * FXL_W + 64 + lane] = t1[k];
+                slum[r * FXL_W + 64 + lane] = luma(rgb(t1[k]));
+            }
         }
     }
     __syncthreads();
     const float FXAA_REDUCE_MIN = 1.0f / 128.0f, FXAA_REDUCE_MUL = 1.0f / 8.0f, FXAA_SPAN_MAX = 8.0f;
     const float ivx = 1.0f / (float)W, ivy = 1.0f / (float)H;  // inverseVP = 1 / u_resolution
     const float k1 = 1.0f / 3.0f - 0.5f, k2 = 2.0f / 3.0f - 0.5f;
-    const int lx = threadIdx.x & 63, x = x0 + lx;
-    // a span tap: post.frag's float address, then the staged texel
+    const int x = x0 + lane;
+    const float fx = ((float)x + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
+    // a span tap: post.frag's float address (NEAREST), then the staged texel
     auto span_tap = [&](float u, float v) -> RGB {
-        const int gx = clamp_med3((int)floorf(u * (float)W), W - 1) - tx0;
-        const int gy = clamp_med3((int)floorf(v * (float)H), H - 1) - ty0;
-        if ((unsigned)gx < (unsigned)FXL_W && (unsigned)gy < (unsigned)FXL_H) return rgb(stex[gy * FXL_W + gx]);
-        return rgb(texel(in, W, H, u, v));
+        const int gx = clamp_to(floor_i32(u * (float)W) - tx0, FXL_W - 1);
+        const int gy = clamp_to(floor_i32(v * (float)H) - ty0, FXL_H - 1);
+        return rgb(stex[gy * FXL_W + gx]);
     };
-    for (int ly = threadIdx.x >> 6; ly < FXL_TY; ly += 4) {
+    for (int ly = wv; ly < FXL_TY; ly += 4) {
         const int y = y0 + ly;
         if (x >= W || y >= H) continue;
         // centre texel (x, H-1-y) in the block
-        const int m = (FXL_TY - 1 - ly + FXL_HALO) * FXL_W + (lx + FXL_HALO);
+        const int m = (FXL_TY - 1 - ly + FXL_HALO) * FXL_W + (lane + FXL_HALO);
         const float lNW = slum[m - FXL_W - 1], lNE = slum[m - FXL_W + 1], lSW = slum[m + FXL_W - 1];
         const float lSE = slum[m + FXL_W + 1], lM = slum[m];
         const uint32_t tM = stex[m];
-        const float fx = ((float)x + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
         const float fy = 1.0f - ((float)y + 0.5f) / (float)H;
-        float lMin = gmin_(lM, gmin_(gmin_(lNW, lNE), gmin_(lSW, lSE)));
-        float lMax = gmax_(lM, gmax_(gmax_(lNW, lNE), gmax_(lSW, lSE)));
+        const float lMin = fminf(lM, fminf(fminf(lNW, lNE), fminf(lSW, lSE)));
+        const float lMax = fmaxf(lM, fmaxf(fmaxf(lNW, lNE), fmaxf(lSW, lSE)));
         float dx = -((lNW + lNE) - (lSW + lSE));
         float dy = ((lNW + lSW) - (lNE + lSE));
-        float dirReduce = gmax_((lNW + lNE + lSW + lSE) * (0.25f * FXAA_REDUCE_MUL), FXAA_REDUCE_MIN);
-        float rcpDirMin = 1.0f / (gmin_(fabsf(dx), fabsf(dy)) + dirReduce);
-        dx = gmin_(FXAA_SPAN_MAX, gmax_(-FXAA_SPAN_MAX, dx * rcpDirMin)) * ivx;
-        dy = gmin_(FXAA_SPAN_MAX, gmax_(-FXAA_SPAN_MAX, dy * rcpDirMin)) * ivy;
+        float dirReduce = fmaxf((lNW + lNE + lSW + lSE) * (0.25f * FXAA_REDUCE_MUL), FXAA_REDUCE_MIN);
+        float rcpDirMin = 1.0f / (fminf(fabsf(dx), fabsf(dy)) + dirReduce);
+        dx = __builtin_amdgcn_fmed3f(dx * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX) * ivx;
+        dy = __builtin_amdgcn_fmed3f(dy * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX) * ivy;
         RGB s1 = span_tap(fx + dx * k1, fy + dy * k1);
         RGB s2 = span_tap(fx + dx * k2, fy + dy * k2);
         RGB a = RGB{(s1.r + s2.r) * 0.5f, (s1.g + s2.g) * 0.5f, (s1.b + s2.b) * 0.5f};
@@ -196,8 +222,10 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
                     a.b * 0.5f + (s3.b + s4.b) * 0.25f};
         float lB = luma(b);
         RGB c = (lB < lMin || lB > lMax) ? a : b;
-        float alpha = (float)(tM >> 24) * (1.0f / 255.0f);
-        out[(size_t)y * W + x] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | (unorm8(alpha) << 24);
+        // (the colour is finite: unorm8 inputs, a correctly rounded, positive rcpDirMin;
+        // alpha stays the texel's own byte: (b / 255) * 255 rounds back to b)
+        out[(size_t)y * W + x] = unorm8_finite(c.r) | (unorm8_finite(c.g) << 8) | (unorm8_finite(c.b) << 16) |
+                                 (tM & 0xff000000u);
     }
 }
 

@@ -67,3 +67,27 @@ def test_no_gpu_means_no_context():
     with pytest.raises(rm.RmError) as e:
         rm.Renderer(0)
     assert e.value.status == 5  # RM_ERR_DEVICE: no silent CPU fallback
+
+
+def test_abi_version_matches_header_and_binding():
+    """include/rm.h RM_ABI_VERSION, librm.so's rm_abi_version() and the ctypes
+    structs of _lib.py describe the same layout (a stale build is refused)."""
+    import ctypes
+    txt = open(os.path.join(ROOT, "include", "rm.h")).read()
+    v = int(re.search(r"#define RM_ABI_VERSION (\d+)", txt).group(1))
+    assert v == _lib.ABI_VERSION == rm.lib().rm_abi_version()
+    # rm_stats: 5 x 8-byte counters/ids + kernel_ms, dispatch, lat_tiles, gather_ms, deinterleave_ms
+    assert ctypes.sizeof(_lib.RmStats) == 56
+    assert [f[0] for f in _lib.RmStats._fields_][-4:] == ["dispatch", "lat_tiles", "gather_ms", "deinterleave_ms"]
+
+
+def test_c_struct_layout_matches_binding(tmp_path):
+    """The C compiler's rm_stats / rm_params layout is the one _lib.py binds."""
+    import ctypes
+    src = tmp_path / "layout.c"
+    src.write_text('#include "rm.h"\n#include <stddef.h>\n'
+                   f'_Static_assert(sizeof(rm_stats) == {ctypes.sizeof(_lib.RmStats)}, "rm_stats");\n'
+                   f'_Static_assert(offsetof(rm_stats, dispatch) == {_lib.RmStats.dispatch.offset}, "dispatch");\n'
+                   f'_Static_assert(offsetof(rm_stats, deinterleave_ms) == {_lib.RmStats.deinterleave_ms.offset}, "d");\n'
+                   f'_Static_assert(sizeof(rm_params) == {ctypes.sizeof(_lib.RmParams)}, "rm_params");\n')
+    subprocess.run(["gcc", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)], check=True)
