@@ -196,11 +196,12 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
         const int gy = clamp_to(floor_i32(v * (float)H) - ty0, FXL_H - 1);
         return rgb(stex[gy * FXL_W + gx]);
     };
-    for (int ly = wv; ly < FXL_TY; ly += 4) {
-        const int y = y0 + ly;
-        if (x >= W || y >= H) continue;
-        // centre texel (x, H-1-y) in the block
-        const int m = (FXL_TY - 1 - ly + FXL_HALO) * FXL_W + (lane + FXL_HALO);
+    // one pixel of row y0 + ly (its value; rows past the frame are computed on a
+    // clamped row and not stored)
+    auto pixel = [&](int ly) -> uint32_t {
+        const int y = min(y0 + ly, H - 1);
+        // centre texel (x, H-1-y) in the block (rows H-1-y-ty0 = TY-1-(y-y0)+HALO)
+        const int m = (FXL_TY - 1 - (y - y0) + FXL_HALO) * FXL_W + (lane + FXL_HALO);
         const float lNW = slum[m - FXL_W - 1], lNE = slum[m - FXL_W + 1], lSW = slum[m + FXL_W - 1];
         const float lSE = slum[m + FXL_W + 1], lM = slum[m];
         const uint32_t tM = stex[m];
@@ -224,8 +225,14 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
         RGB c = (lB < lMin || lB > lMax) ? a : b;
         // (the colour is finite: unorm8 inputs, a correctly rounded, positive rcpDirMin;
         // alpha stays the texel's own byte: (b / 255) * 255 rounds back to b)
-        out[(size_t)y * W + x] = unorm8_finite(c.r) | (unorm8_finite(c.g) << 8) | (unorm8_finite(c.b) << 16) |
-                                 (tM & 0xff000000u);
+        return unorm8_finite(c.r) | (unorm8_finite(c.g) << 8) | (unorm8_finite(c.b) << 16) | (tM & 0xff000000u);
+    };
+    // two rows at a time: their dependent chains (LDS taps -> division -> span
+    // taps) interleave
+    for (int ly = wv; ly < FXL_TY; ly += 8) {
+        const uint32_t v0 = pixel(ly), v1 = pixel(ly + 4);
+        if (x < W && y0 + ly < H) out[(size_t)(y0 + ly) * W + x] = v0;
+        if (x < W && y0 + ly + 4 < H) out[(size_t)(y0 + ly + 4) * W + x] = v1;
     }
 }
 

@@ -413,147 +413,6 @@ __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRa
     return soft_shadow2_T_loop<true, NB, ST>(F, s, mint, maxt, cnt);
 }
 
-// ---- The cooperative tail of scene T's soft shadow (the latency tiles).
-// A latency tile's wave ends with a few lanes marching grazing shadows of
-// hundreds of dependent steps while its other lanes are done: the launch's
-// (and a C4 share's) last waves are such chains.  A VALU instruction costs a
-// wave its issue slot whatever its active lanes, so idle lanes are free
-// helpers: once at most 16 lanes still march (checked every 16 steps), each
-// remaining march moves to a quad of lanes, lane k of the quad computing
-// Menger fold k (lane 3 repeats fold 0), and the quad combines them with two
-// DPP maxima.  A step issues about half the instructions of the one-lane
-// step.  Same operations on the same values: every fold value is the one
-// sponge_folds forms, and d = max(box, c0, c1, c2) by IEEE maximum is exact
-// in any order (a fold past its exit point is <= d, which is why the one-lane
-// loop may skip it), so h, num, den, P and t, and the frame, are bit-identical
-// (the instrumented kernels run the one-lane loop; tests compare the frames).
-struct ShadowT {  // one soft-shadow march of soft_shadow2_T_loop (SM 0, uncapped), resumable
-    LinRay s;
-    float t, maxt, num, den, P, h;
-    int it;
-};
-__device__ __forceinline__ ShadowT shadow_T_init(const LinRay& s, float mint, float maxt) {
-    return ShadowT{s, mint, maxt, 1.0f / 16.0f, 1.0f, 0.0f, 1.0f, 1};
-}
-// one step of soft_shadow2_T_loop's body on distance h; true while the march
-// goes on.  FIRST: the march's first step may be this one (it == 1: Q = 1, D = t)
-template <bool FIRST = true>
-__device__ __forceinline__ bool shadow_T_step(ShadowT& S, float h) {
-    S.h = h;
-    const float h2 = h * h;
-    const float Q = FIRST && S.it == 1 ? 1.0f : fmaf(S.P, S.P, -h2);
-    const float D = FIRST && S.it == 1 ? S.t : fmaf(S.t, S.P, -h2);
-    const float cn = h2 * Q, cd = D * fabsf(D);
-    const bool upd = (Q >= 0.0f) & (cn * S.den < S.num * cd);
-    S.num = upd ? cn : S.num;
-    S.den = upd ? cd : S.den;
-    S.P = h + h;
-#if RM_SHADOW_P_PIN
-    asm volatile("" : "+v"(S.P));
-#endif
-    S.t = fmaf(h, 0.1f, S.t + 0.001f);
-    S.it++;
-    return !((h < 0.001f) | !(S.t < S.maxt));
-}
-__device__ __forceinline__ float shadow_T_result(const ShadowT& S) {
-    return S.h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(16.0f * S.num * __builtin_amdgcn_rcpf(S.den));
-}
-// one-lane steps (NB fold tests); with `handoff`, returns early (true) once at
-// most kCoopLanes lanes of the wave still march; false when this march is done
-#ifndef RM_COOP_LANES
-#define RM_COOP_LANES 16
-#endif
-#ifndef RM_COOP_MIN_IT  // steps a march has taken before it may be handed off
-#define RM_COOP_MIN_IT 64
-#endif
-#ifndef RM_COOP_HANDOFF  // 0: the restructured loop without hand-offs (A/B of its overhead)
-#define RM_COOP_HANDOFF 1
-#endif
-#ifndef RM_COOP_FOLD_SKIP
-#define RM_COOP_FOLD_SKIP 0
-#endif
-constexpr int kCoopLanes = RM_COOP_LANES;
-template <int NB>
-__device__ __forceinline__ bool shadow_T_run(ShadowT& S, bool handoff) {
-    if (S.it == 1 && !(S.t < S.maxt)) return false;
-    uint32_t fl = 0;
-    // the wave's step count: every lane still here has taken as many steps as
-    // the loop has run (wave-uniform inside the loop: a scalar counter)
-    for (int n = 1;; n++) {
-        const V3 q = at(S.s, S.t);
-        if (!shadow_T_step(S, sponge_folds<false, NB>(q, sponge_box(q), fl))) return false;
-        if (RM_COOP_HANDOFF && handoff && (n & 15) == 0 && n >= RM_COOP_MIN_IT &&
-            __popcll(__builtin_amdgcn_ballot_w64(true)) <= kCoopLanes)
-            return true;
-    }
-}
-__device__ __forceinline__ float dpp_quad_max(float d) {
-    const int a = __builtin_amdgcn_mov_dpp(__float_as_int(d), 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    d = __builtin_elementwise_maximum(d, __int_as_float(a));
-    const int b = __builtin_amdgcn_mov_dpp(__float_as_int(d), 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    return __builtin_elementwise_maximum(d, __int_as_float(b));
-}
-// The quads' march: every lane of a full wave calls it; `pending` lanes are the
-// marches handed off (at most kCoopLanes).  Quad g takes the g-th of them and
-// its lane receives the result in S.
-__device__ __forceinline__ void shadow_T_coop(ShadowT& S, bool pending) {
-    const uint64_t pend = __builtin_amdgcn_ballot_w64(pending);
-    const int lane = (int)__lane_id(), g = lane >> 2, k = lane & 3;
-    int src = 0;  // lane of the g-th pending march
-    uint64_t m = pend;
-    for (int i = 0; i < kCoopLanes && m; i++) {
-        const int b = __builtin_ctzll(m);
-        src = g == i ? b : src;
-        m &= m - 1;
-    }
-    ShadowT C;
-    C.s.o = v3(__shfl(S.s.o.x, src), __shfl(S.s.o.y, src), __shfl(S.s.o.z, src));
-    C.s.d = v3(__shfl(S.s.d.x, src), __shfl(S.s.d.y, src), __shfl(S.s.d.z, src));
-    C.t = __shfl(S.t, src); C.maxt = __shfl(S.maxt, src);
-    C.num = __shfl(S.num, src); C.den = __shfl(S.den, src);
-    C.P = __shfl(S.P, src); C.h = __shfl(S.h, src); C.it = __shfl(S.it, src);
-    // fold k of sponge_folds' fast form (lane 3 repeats fold 0: the quad's
-    // maximum is the same)
-    const float SH = k == 1 ? 1.5f : k == 2 ? 4.5f : 0.5f, INV = k == 1 ? 1.0f / 9.0f : k == 2 ? 1.0f / 27.0f : 1.0f / 3.0f;
-    if (g < __popcll(pend)) {
-        for (;;) {
-            const V3 q = at(C.s, C.t);
-            float d = sponge_box(q);
-            // RM_COOP_FOLD_SKIP: folds only where a march needs one (box < 1/3:
-            // fold 0's exit test; wave-uniform, as sponge_folds' tests)
-            if (!RM_COOP_FOLD_SKIP || __builtin_amdgcn_ballot_w64(d < 1.0f / 3.0f) != 0) {
-                const float yx = fmaf(q.x, SH, -0.5f), yy = fmaf(q.y, SH, -0.5f), yz = fmaf(q.z, SH, -0.5f);
-                const float gx = yx - __builtin_rintf(yx), gy = yy - __builtin_rintf(yy), gz = yz - __builtin_rintf(yz);
-                const float rx = fabsf(fmaf(-6.0f, fabsf(gx), 1.0f)), ry = fabsf(fmaf(-6.0f, fabsf(gy), 1.0f));
-                const float rz = fabsf(fmaf(-6.0f, fabsf(gz), 1.0f));
-                const float c = fmaf(__builtin_amdgcn_fmed3f(rx, ry, rz), INV, -INV);
-                d = dpp_quad_max(__builtin_elementwise_maximum(c, d));
-            }
-            // (a handed-off march is past its first step: it >= 16)
-            if (!shadow_T_step<false>(C, d)) break;
-        }
-    }
-    // each handed-off march takes its result back from lane 0 of its quad
-    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pend >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pend, 0u));
-    const float h = __shfl(C.h, 4 * rank), num = __shfl(C.num, 4 * rank), den = __shfl(C.den, 4 * rank);
-    if (pending) {
-        S.h = h;
-        S.num = num;
-        S.den = den;
-    }
-}
-// soft_shadow2_T_loop<false, NB, 0> for lanes with `lit`, with the cooperative
-// tail when every lane of the wave is here (a full tile)
-template <int NB>
-__device__ __forceinline__ float soft_shadow2_T_coop(const LinRay& s, float mint, float maxt, bool lit) {
-    ShadowT S = shadow_T_init(s, mint, maxt);
-    const bool full = __builtin_amdgcn_ballot_w64(true) == ~0ull;
-    bool pending = false;
-    if (lit) pending = shadow_T_run<NB>(S, full);
-    if (full && __builtin_amdgcn_ballot_w64(pending) != 0) shadow_T_coop(S, pending);
-    return lit ? shadow_T_result(S) : 1.0f;
-}
-
 // castRay (common.frag:931-954) for scene T in sponge space; returns the
 // depth of the point the reference returns (ZFAR on escape).  depth < ZFAR
 // holds at a hit and after step exhaustion, so the escape value is set once,
@@ -835,9 +694,6 @@ __device__ __forceinline__ V3 render_O(const FrameConst& F, V3 ro, V3 rd, Tally&
 
 // template.frag:45-76 (scene T); NB: sponge_folds; SETTLE: soft_shadow2_T_loop;
 // RSTOP: cast_ray_T's RS for the reflection march
-#ifndef RM_LAT_COOP
-#define RM_LAT_COOP 1
-#endif
 template <int NB = 3, int SETTLE = 0, int RSTOP = 0>
 __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally& cnt) {
     constexpr int SC = SCENE_T;
@@ -860,18 +716,9 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
 #ifdef RM_ABLATE_SHADOW
     float sha = 1.0f;
 #else
-    float sha;
-    // the timed latency tiles (NB 1, no settle exit, backface skip): the
-    // cooperative tail (soft_shadow2_T_coop) for the reference's uncapped loop
-    constexpr bool kCoop = RM_LAT_COOP && NB == 1 && SETTLE == 0 && RSTOP == 1;
-    if (kCoop && F.shadow_max_steps == __INT_MAX__) {
-        sha = soft_shadow2_T_coop<NB>(sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2),
-                                      !(dot(lightDir, n) < 0.0f));
-    } else {
-        sha = shadow_if_lit<RSTOP>(dot(lightDir, n), cnt, [&] {
-            return soft_shadow2_T<NB, SETTLE>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
-        });
-    }
+    float sha = shadow_if_lit<RSTOP>(dot(lightDir, n), cnt, [&] {
+        return soft_shadow2_T<NB, SETTLE>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
+    });
 #endif
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));

@@ -15,6 +15,13 @@ CONFIGS = [  # name, scene, W, H, steps, pose, band, nshards, shard
     ("O4096", "O", 4096, 4096, 512, "P0", 4096, 1, 0),
     ("C5frame", "O", 8192, 8192, 512, "P0", 8192, 1, 0),
     ("C5share", "O", 8192, 8192, 512, "P0", 16, 8, 0),
+    # other poses (select with CONFIGS=...)
+    ("C2P0", "T", 1920, 1080, 128, "P0", 1080, 1, 0),
+    ("C2P3", "T", 1920, 1080, 128, "P3", 1080, 1, 0),
+    ("C2P8", "T", 1920, 1080, 128, "P8", 1080, 1, 0),
+    ("C4shareP1", "T", 4096, 4096, 256, "P1", 16, 8, 0),
+    ("C4shareP3", "T", 4096, 4096, 256, "P3", 16, 8, 0),
+    ("C4share7", "T", 4096, 4096, 256, "P0", 16, 8, 7),
 ]
 
 CHILD = r'''
