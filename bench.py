@@ -62,6 +62,11 @@ def parse():
     ap.add_argument("--max-steps", type=int, default=256)
     ap.add_argument("--pose", default="P0")
     ap.add_argument("--band", type=int, default=16)
+    ap.add_argument("--balance", default="auto", choices=["auto", "even"],
+                    help="N > 1: 'even' deals rows in round-robin bands of --band; 'auto' also measures a "
+                         "split that gives rank 0 (which receives every other rank's rows and de-interleaves) "
+                         "a longer run per cycle, sized from the timed exchange, and keeps whichever plan ran "
+                         "the untimed trial frames faster")
     ap.add_argument("--chunks", type=int, default=None,
                     help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
@@ -255,6 +260,27 @@ def time_bloom(r, frame8, stream, reps=20):
             "mip_levels": d2, "texel_fetches_per_px": 4 * (1 + 25 * 2)}
 
 
+def balanced_runs(world, band, H, ex):
+    """Rows per cycle for each rank from one even-split timed exchange, per-rank
+    lists of render_ms / pack_ms and rank 0's gather_ms / deinterleave_ms.
+    With every rank rendering 1/N of the rows, the frame costs T1 = sum of the
+    renders on one GPU and G = N * gather_ms to move whole through one link
+    (each non-root rank's rows cross their own xGMI link, concurrently).  A
+    non-root rank with share s is busy s * max(T1, G) per pipelined frame (its
+    render and its send overlap); rank 0 is busy s0 * T1 + de-interleave, with
+    s0 = 1 - (N - 1) s.  Equal busy times give
+        s = (T1 + d) / (max(T1, G) + (N - 1) T1),
+    and rank 0's run is band * s0 / s (the others keep `band`), capped so that a
+    cycle fits twice in the frame (every rank keeps rows)."""
+    T1 = sum(ex["render_ms"])
+    G = world * ex["gather_ms"]
+    d = ex["deinterleave_ms"]
+    s = (T1 + d) / (max(T1, G) + (world - 1) * T1)
+    s0 = max(1.0 - (world - 1) * s, 0.0)
+    r0 = int(min(max(round(band * s0 / s), 1), max(1, H // 2 - (world - 1) * band)))
+    return [r0] + [band] * (world - 1), dict(T1_ms=T1, G_ms=G, deinterleave_ms=d, share_other=s, share_root=s0)
+
+
 def roofline(pmc, flop_tally, evals, ref_flop_per_step, kern_ms, out_bytes):
     """The render kernel's FP32-VALU roofline.  With PMC counters of this
     workload (profiles/pmc_counters.json, rocprofv3 --pmc of the same command):
@@ -338,6 +364,78 @@ def main():
     r.set_stream(stream)
     chunks = args.chunks if args.chunks is not None else 1
     fr = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks, streams=args.streams)
+    red_dev = dev if args.backend == "nccl" else torch.device("cpu")
+
+    def spin_up():
+        # a fresh GPU ramps its clocks over the first ~0.1 s of load.  Every rank
+        # runs the same number of rounds (each frame holds a gather), so whether
+        # to go on is agreed over all ranks after each round.
+        t_spin = time.perf_counter()
+        while args.spinup > 0:
+            for _ in range(8):
+                fr.submit()
+            fr.flush()
+            torch.cuda.synchronize(dev)
+            go = torch.tensor([1.0 if time.perf_counter() - t_spin < args.spinup else 0.0], device=red_dev)
+            if world > 1:
+                dist.all_reduce(go, op=dist.ReduceOp.MIN)
+            if go.item() == 0.0:
+                break
+
+    def trial_ms(f, n=16):
+        # untimed trial: n pipelined frames, wall time, max over ranks
+        for _ in range(4):
+            f.submit()
+        f.flush()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(n):
+            f.submit()
+        f.flush()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tt = torch.tensor([(time.perf_counter() - t1) / n * 1e3], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    balance = None
+    if world > 1 and args.balance == "auto" and args.fmt == "rgba8":
+        # split calibration (untimed): one timed exchange of the even split,
+        # the balanced runs it implies, then trial frames of both plans
+        spin_up()
+        xs = [fr.timed_exchange() for _ in range(3)]
+        mine = torch.tensor([_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
+                                                                    "deinterleave_ms")],
+                            dtype=torch.float64, device=red_dev)
+        per = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(per, mine)
+        per = [[float(v) for v in x.cpu()] for x in per]
+        ex = {"render_ms": [x[0] for x in per], "pack_ms": [x[1] for x in per], "gather_ms": per[0][2],
+              "deinterleave_ms": per[0][3]}
+        runs, model = balanced_runs(world, args.band, H, ex)
+        even_ms = trial_ms(fr)
+        bal, bal_ms, err = None, float("inf"), None
+        try:
+            bal = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks,
+                                   streams=args.streams, runs=runs)
+            bal_ms = trial_ms(bal)
+        except (RuntimeError, ValueError) as e:  # keep the even split; say why in the line
+            err = f"{type(e).__name__}: {e}"
+            torch.cuda.synchronize(dev)
+        chosen = "balanced" if bal_ms < even_ms else "even"
+        balance = {"mode": "auto", "chosen": chosen, "runs": runs if chosen == "balanced" else [args.band] * world,
+                   "trial_ms": {"even": even_ms, "balanced": bal_ms}, "balanced_runs": runs, "model": model,
+                   "note": "untimed trial frames (16 pipelined frames per plan, max over ranks) before the "
+                           "instrumented run and the warm-up; the timed frames use the chosen plan"}
+        if err is not None:
+            balance["error"] = err
+        if chosen == "balanced":
+            fr = bal
+        else:
+            del bal
+    elif world > 1:
+        balance = {"mode": "even", "chosen": "even", "runs": [args.band] * world}
 
     def set_frame(i):  # walk: the pose of frame i (timed frames 0..K-1)
         if args.walk:
@@ -356,7 +454,6 @@ def main():
     if args.walk:
         st = dict(st, evals=sum(walk_evals) / len(walk_evals), skipped=sum(walk_skipped) / len(walk_skipped))
     r.set_params(count_evals=0)
-    red_dev = dev if args.backend == "nccl" else torch.device("cpu")
     ev_rank = torch.tensor([st["evals"], st.get("skipped", 0)], dtype=torch.float64, device=red_dev)
     ev_total = ev_rank.clone()
     if world > 1:
@@ -367,20 +464,8 @@ def main():
     # untimed spin-up before the W warm-up frames: a fresh GPU ramps its clocks
     # over the first ~0.1 s of load (3 warm-up frames are ~3 ms), so the timed
     # frames would otherwise include the ramp.  Same frames, same work.
-    # Every rank runs the same number of rounds (each frame holds a gather), so
-    # whether to go on is agreed over all ranks after each round.
-    t_spin = time.perf_counter()
     set_frame(-args.warmup)
-    while args.spinup > 0:
-        for _ in range(8):
-            fr.submit()
-        fr.flush()
-        torch.cuda.synchronize(dev)
-        go = torch.tensor([1.0 if time.perf_counter() - t_spin < args.spinup else 0.0], device=red_dev)
-        if world > 1:
-            dist.all_reduce(go, op=dist.ReduceOp.MIN)
-        if go.item() == 0.0:
-            break
+    spin_up()
     for i in range(-args.warmup, 0):
         set_frame(i)
         fr.submit()
@@ -436,6 +521,7 @@ def main():
         # each timed alone after the timed region: the gather's own time, which
         # the pipelined frames overlap with the next frame's render
         xs = [fr.timed_exchange() for _ in range(5)]
+        wire_row = fr.wires[0].stride(0) * fr.wires[0].element_size()  # bytes of one row on the wire
         mine = torch.tensor([kern] + [_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
                                                                                 "deinterleave_ms")],
                             dtype=torch.float64, device=red_dev)
@@ -446,8 +532,8 @@ def main():
             "gather_ms": pr[0][3], "deinterleave_ms": pr[0][4], "pack_ms": pr[0][2],
             "kernel_ms_per_rank": [x[0] for x in pr], "gather_ms_per_rank": [x[3] for x in pr],
             "pack_ms_per_rank": [x[2] for x in pr],
-            "wire_bytes_per_rank": fr.wires[0].numel() * fr.wires[0].element_size(),
-            "root_ingress_bytes": (world - 1) * fr.wires[0].numel() * fr.wires[0].element_size(),
+            "wire_bytes_per_rank": [fr.plan.count(q) * wire_row for q in range(world)],
+            "root_ingress_bytes": sum(fr.plan.count(q) for q in range(1, world)) * wire_row,
             "backend": args.backend,
             "note": "median of 5 frames whose steps run one after another, each timed alone after the timed "
                     "region: kernel_ms_per_rank = each rank's render kernel (11 synchronous launches), "
@@ -491,7 +577,10 @@ def main():
             "config": {
                 "workload": f"{_config_id(args.scene, W, H, args.max_steps, world)}: {W}x{H} scene {args.scene} "
                             f"({rm.SCENE_FILES[args.scene]}), {args.max_steps} max steps, pose {args.pose}, "
-                            f"row bands of {args.band} over {world} GPU(s), {args.fmt} frame on rank 0"
+                            + (f"row bands of {args.band} over {world} GPU(s)" if fr.plan.runs is None else
+                               f"weighted row runs {list(fr.plan.runs)} per cycle of {fr.plan.cycle} over "
+                               f"{world} GPUs")
+                            + f", {args.fmt} frame on rank 0"
                             + (f", walking (camera +{args.walk_speed}/frame forward, u_time +{args.walk_dt:.4f} s/frame)"
                                if args.walk else ""),
                 "scene": args.scene, "W": W, "H": H, "max_steps": args.max_steps, "pose": args.pose,
@@ -517,6 +606,8 @@ def main():
             "roofline": roof,
             "frame_check": check,
         }
+        if balance is not None:
+            res["balance"] = balance
         if exchange is not None:
             res.update(exchange)
         if fr.frame is not None and fr.fmt == "rgba8":

@@ -266,6 +266,27 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
  * context's stream. */
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
 
+/* ---- Weighted row parts: frame row y belongs to a part iff (y mod cycle) - offset
+ * lies in [0, run).  Round-robin bands are the special case run = band,
+ * cycle = band * nshards, offset = band * shard; parts with different runs give
+ * ranks different shares of every cycle (bench.py's balanced multi-GPU split:
+ * the root, which receives the others' rows, renders a longer run).
+ * rm_cycle_rows: the number of frame rows of a part.  rm_render_cycle_rows[_rgba8]:
+ * the part's packed rows [row_begin, row_begin + row_count) in increasing y,
+ * as rm_render_rows[_rgba8].  rm_deinterleave_cycle_rgb8: the root side, the
+ * W x H RGBA8 frame (alpha 255) from nparts parts that tile [0, cycle) in
+ * order (offsets[i + 1] = offsets[i] + runs[i]), part i's packed 3 B/px rows
+ * starting at byte part_bytes[i] of `gathered` (device pointers, ctx stream;
+ * nparts <= 64). */
+rm_status rm_cycle_rows(int H, int cycle, int offset, int run, int *nrows);
+rm_status rm_render_cycle_rows(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int row_begin,
+                               int row_count, float *out, rm_stats *stats);
+rm_status rm_render_cycle_rows_rgba8(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int row_begin,
+                                     int row_count, uint32_t *out, rm_stats *stats);
+rm_status rm_deinterleave_cycle_rgb8(rm_ctx *ctx, int W, int H, int cycle, int nparts, const int *offsets,
+                                     const int *runs, const int64_t *part_bytes, const uint8_t *gathered,
+                                     uint32_t *out);
+
 /* ---- Multi-GPU: row-sharded frames over RCCL ----
  * The reference renders one frame on one GPU (main.cpp:196-207); here a frame's
  * rows are dealt to nranks GPUs in bands of `band` rows, round robin (rank r

@@ -190,6 +190,40 @@ class Renderer:
                  self._ptr(out), ctypes.byref(s) if stats else None), self._ctx)
         return (out, s.as_dict()) if stats else out
 
+    def render_cycle_rows(self, W, H, cycle, offset, run, row_begin, row_count, out, stats=False):
+        """Packed rows [row_begin, row_begin + row_count) of the cyclic part
+        (y mod cycle) - offset in [0, run), as render_rows (float32 or RGBA8 out)."""
+        torch = _torch()
+        rgba8 = out.dtype != torch.float32
+        _check_out(out, row_count * W * (1 if rgba8 else 4))
+        s = RmStats()
+        fn = lib().rm_render_cycle_rows_rgba8 if rgba8 else lib().rm_render_cycle_rows
+        check(fn(self._ctx, int(W), int(H), int(cycle), int(offset), int(run), int(row_begin), int(row_count),
+                 self._ptr(out), ctypes.byref(s) if stats else None), self._ctx)
+        return (out, s.as_dict()) if stats else out
+
+    def deinterleave_cycle_rgb8(self, W, H, cycle, offsets, runs, part_bytes, gathered, out=None):
+        """The RGBA8 frame (alpha 255) from cyclic parts' packed RGB8 rows:
+        part i (offsets[i], runs[i], tiling [0, cycle) in order) starts at byte
+        part_bytes[i] of the contiguous uint8 `gathered`."""
+        torch = _torch()
+        n = len(offsets)
+        if len(runs) != n or len(part_bytes) != n:
+            raise ValueError("deinterleave_cycle_rgb8: offsets, runs and part_bytes differ in length")
+        if gathered.dtype != torch.uint8 or not gathered.is_contiguous():
+            raise ValueError("deinterleave_cycle_rgb8: gathered must be a contiguous uint8 tensor")
+        for o, r, b in zip(offsets, runs, part_bytes):
+            if b + cycle_rows(H, cycle, o, r) * 3 * W > gathered.numel():
+                raise ValueError("deinterleave_cycle_rgb8: a part's rows run past the end of gathered")
+        if out is None:
+            out = torch.empty((H, W), dtype=torch.int32, device=gathered.device)
+        _check_out(out, H * W)
+        check(lib().rm_deinterleave_cycle_rgb8(self._ctx, int(W), int(H), int(cycle), n,
+                                               (ctypes.c_int * n)(*offsets), (ctypes.c_int * n)(*runs),
+                                               (ctypes.c_int64 * n)(*part_bytes), self._ptr(gathered),
+                                               self._ptr(out)), self._ctx)
+        return out
+
     def render_band_rgba8(self, W, H, band, nshards, shard, out=None, stats=False):
         """render_band into RGBA8 words ([rows, W] int32)."""
         torch = _torch()
@@ -406,6 +440,13 @@ def _check_out(t, nfloats):
         ok, n, es = bool(t.flags["C_CONTIGUOUS"]), t.size, t.itemsize
     if not ok or n < nfloats or es != 4:
         raise ValueError(f"buffer must be contiguous 32-bit with >= {nfloats} elements")
+
+
+def cycle_rows(H: int, cycle: int, offset: int, run: int) -> int:
+    """Frame rows y < H with (y mod cycle) - offset in [0, run) (rm_cycle_rows)."""
+    n = ctypes.c_int()
+    check(lib().rm_cycle_rows(int(H), int(cycle), int(offset), int(run), ctypes.byref(n)))
+    return n.value
 
 
 def shard_rows(H: int, band: int, nshards: int, shard: int) -> int:

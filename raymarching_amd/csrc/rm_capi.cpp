@@ -343,7 +343,30 @@ int sched_dilate() {
     return n;
 }
 
-FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int shard, int nrows) {
+// The frame rows one launch renders: y with (y mod cycle) - offset in [0, run)
+// (round-robin bands: run = band, cycle = band * nshards, offset = band * shard).
+struct RowPart {
+    int cycle, offset, run;
+};
+// validated row part of round-robin bands, or of an explicit cyclic part
+bool band_part(int band, int nshards, int shard, RowPart &p) {
+    if (band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards || (long long)band * nshards > 0x7fffffffLL) return false;
+    p = RowPart{band * nshards, band * shard, band};
+    return true;
+}
+bool cycle_part(int cycle, int offset, int run, RowPart &p) {
+    if (cycle <= 0 || offset < 0 || run <= 0 || (long long)offset + run > cycle) return false;
+    p = RowPart{cycle, offset, run};
+    return true;
+}
+int rows_of_part(int H, const RowPart &p) {
+    const long long full = H / p.cycle, rest = H - full * p.cycle;
+    long long tail = rest - p.offset;
+    tail = tail < 0 ? 0 : tail > p.run ? p.run : tail;
+    return (int)(full * p.run + tail);
+}
+
+FrameConst frame_const(const rm_ctx *c, int W, int H, const RowPart &part, int nrows) {
     FrameConst F;
     std::memset(&F, 0, sizeof(F));
     F.res_x = c->res_set ? c->res[0] : (float)W;
@@ -360,7 +383,7 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int
     F.ry_c = rm::glsl_cos(ay); F.ry_s = rm::glsl_sin(ay);
     F.rx_c = rm::glsl_cos(ax); F.rx_s = rm::glsl_sin(ax);
     F.W = W; F.H = H;
-    F.band = band; F.nshards = nshards; F.shard = shard; F.nrows = nrows;
+    F.cycle = part.cycle; F.offset = part.offset; F.run = part.run; F.nrows = nrows;
     F.time = c->time;
     F.mouse_x = c->mouse[0];
     F.mouse_y = c->mouse[1];
@@ -377,11 +400,8 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, int band, int nshards, int
 }
 
 int rows_of_shard(int H, int band, int nshards, int shard) {
-    int nbands = (H + band - 1) / band;
-    int n = 0;
-    // bands shard, shard + nshards, ...; the last band may be short
-    for (int b = shard; b < nbands; b += nshards) n += (b == nbands - 1) ? H - b * band : band;
-    return n;
+    RowPart p;
+    return band_part(band, nshards, shard, p) ? rows_of_part(H, p) : 0;
 }
 
 rm_status ensure_staging(rm_ctx *ctx, size_t bytes) {
@@ -420,8 +440,7 @@ hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
 
 // The adaptive-order state of a launch geometry on the ctx stream (least
 // recently used entry recycled), or null when scheduling does not apply.
-rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count,
-                          rm_status &st) {
+rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, int count, rm_status &st) {
     st = RM_OK;
     // plugins always launch one-wave 8x8 tiles (rm_plugin_kernels.h)
     if (!ctx->params.schedule ||
@@ -430,8 +449,8 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
     const rm::TileGrid g = rm::tile_grid(rm::KERNEL_TILE8, W, count);
     const int n = g.x * g.y;
     uint64_t key = 0xcbf29ce484222325ULL;
-    for (long long v : {(long long)ctx->scene, (long long)W, (long long)H, (long long)band, (long long)nshards,
-                        (long long)shard, (long long)row0, (long long)count})
+    for (long long v : {(long long)ctx->scene, (long long)W, (long long)H, (long long)part.cycle, (long long)part.offset,
+                        (long long)part.run, (long long)row0, (long long)count})
         key = (key ^ (uint64_t)v) * 0x100000001b3ULL;
     rm_ctx::Sched *lru = &ctx->sched[0];
     for (rm_ctx::Sched &e : ctx->sched) {
@@ -461,10 +480,10 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, int band, int nshards, int 
     return lru;
 }
 
-rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row0, int count, void *out,
-                     bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
+rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, int count, void *out, bool rgba8,
+                     rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
     rm::TraceRange range("rm_render");
-    FrameConst F = frame_const(ctx, W, H, band, nshards, shard, count);
+    FrameConst F = frame_const(ctx, W, H, part, count);
     F.row0 = row0;
     F.evals_map = evmap;
     if (accum) {  // fract(u_seed1) - 0.5 (GLSL fract, x - floor(x)), per frame
@@ -480,7 +499,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
         if ((int64_t)g.x * g.y == ctx->tile_order_n) F.tile_order = ctx->tile_order;
     } else {
         rm_status st;
-        sc = sched_slot(ctx, W, H, band, nshards, shard, row0, count, st);
+        sc = sched_slot(ctx, W, H, part, row0, count, st);
         if (st != RM_OK) return st;
         if (sc) {
             const uint64_t P = (uint64_t)sched_period(), k = sc->k;
@@ -558,16 +577,15 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
 }
 
 // row_count < 0: every packed row from row_begin on; out: float4 or RGBA8 rows
-rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
-                     void *out, bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
+rm_status render_part(rm_ctx *ctx, int W, int H, const RowPart &part, int row_begin, int row_count, void *out,
+                      bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
-    if (W <= 0 || H <= 0 || band <= 0 || nshards <= 0 || shard < 0 || shard >= nshards)
-        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
+    if (W <= 0 || H <= 0) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size");
     if ((long long)W * H > (1LL << 31)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: frame too large");
     if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
     if (ctx->scene == rm::SCENE_PLUGIN && !ctx->plugin.render)
         return fail(ctx, RM_ERR_SCENE, "scene plugin was compiled with RM_PLUGIN_EVAL_ONLY (no render kernel)");
-    int n = rows_of_shard(H, band, nshards, shard);
+    int n = rows_of_part(H, part);
     if (row_count < 0) row_count = n - row_begin;
     if (row_begin < 0 || row_count < 0 || row_begin + row_count > n)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: packed row range outside the shard");
@@ -582,7 +600,7 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     RM_HIP(hipSetDevice(ctx->device));
     const bool dev_out = is_device_ptr(out), dev_map = !evmap || is_device_ptr(evmap);
     if (dev_out && dev_map)
-        return render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, out, rgba8, stats, evmap, accum);
+        return render_dev(ctx, W, H, part, row_begin, row_count, out, rgba8, stats, evmap, accum);
     // host buffers go through the staging buffer: the frame, then the step map
     const size_t bytes = dev_out ? 0 : (size_t)W * row_count * (rgba8 ? sizeof(uint32_t) : sizeof(float4));
     const size_t map_bytes = dev_map ? 0 : (size_t)W * row_count * sizeof(uint32_t);
@@ -591,13 +609,22 @@ rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard
     char *st = reinterpret_cast<char *>(ctx->staging);
     uint32_t *map_d = dev_map ? evmap : reinterpret_cast<uint32_t *>(st + bytes);
     if (accum && !dev_out) RM_HIP(hipMemcpyAsync(st, out, bytes, hipMemcpyHostToDevice, ctx->stream));  // u_sample
-    s = render_dev(ctx, W, H, band, nshards, shard, row_begin, row_count, dev_out ? out : st, rgba8, stats, map_d,
-                   accum);
+    s = render_dev(ctx, W, H, part, row_begin, row_count, dev_out ? out : st, rgba8, stats, map_d, accum);
     if (s != RM_OK) return s;
     if (!dev_out) RM_HIP(hipMemcpyAsync(out, st, bytes, hipMemcpyDeviceToHost, ctx->stream));
     if (!dev_map) RM_HIP(hipMemcpyAsync(evmap, map_d, map_bytes, hipMemcpyDeviceToHost, ctx->stream));
     RM_HIP(hipStreamSynchronize(ctx->stream));
     return RM_OK;
+}
+
+// round-robin bands (band, nshards, shard)
+rm_status render_any(rm_ctx *ctx, int W, int H, int band, int nshards, int shard, int row_begin, int row_count,
+                     void *out, bool rgba8, rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    RowPart part;
+    if (W <= 0 || H <= 0 || !band_part(band, nshards, shard, part))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "render: bad size/shard");
+    return render_part(ctx, W, H, part, row_begin, row_count, out, rgba8, stats, evmap, accum);
 }
 
 }  // namespace
@@ -877,6 +904,60 @@ rm_status rm_render_rows_rgba8(rm_ctx *ctx, int W, int H, int band, int nshards,
     return render_any(ctx, W, H, band, nshards, shard, row_begin, row_count, out, true, stats);
 }
 
+rm_status rm_cycle_rows(int H, int cycle, int offset, int run, int *nrows) {
+    RowPart p;
+    if (!nrows || H <= 0 || !cycle_part(cycle, offset, run, p)) return RM_ERR_INVALID_ARGUMENT;
+    *nrows = rows_of_part(H, p);
+    return RM_OK;
+}
+
+rm_status rm_render_cycle_rows(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int row_begin,
+                               int row_count, float *out, rm_stats *stats) {
+    RowPart p;
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!cycle_part(cycle, offset, run, p) || row_count < 0)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_cycle_rows: bad cycle/offset/run/row_count");
+    return render_part(ctx, W, H, p, row_begin, row_count, out, false, stats);
+}
+
+rm_status rm_render_cycle_rows_rgba8(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int row_begin,
+                                     int row_count, uint32_t *out, rm_stats *stats) {
+    RowPart p;
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!cycle_part(cycle, offset, run, p) || row_count < 0)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_cycle_rows_rgba8: bad cycle/offset/run/row_count");
+    return render_part(ctx, W, H, p, row_begin, row_count, out, true, stats);
+}
+
+rm_status rm_deinterleave_cycle_rgb8(rm_ctx *ctx, int W, int H, int cycle, int nparts, const int *offsets,
+                                     const int *runs, const int64_t *part_bytes, const uint8_t *gathered,
+                                     uint32_t *out) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (W <= 0 || H <= 0 || cycle <= 0 || nparts < 1 || nparts > rm::kMaxCycleParts || !offsets || !runs ||
+        !part_bytes || !gathered || !out)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave_cycle_rgb8: bad arguments");
+    rm::CycleParts parts;
+    std::memset(&parts, 0, sizeof(parts));
+    parts.n = nparts;
+    int next = 0;  // the parts, in order, tile [0, cycle)
+    for (int i = 0; i < nparts; i++) {
+        RowPart p;
+        if (offsets[i] != next || !cycle_part(cycle, offsets[i], runs[i], p) || part_bytes[i] < 0)
+            return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave_cycle_rgb8: parts must tile [0, cycle) in order");
+        next += runs[i];
+        parts.off[i] = offsets[i];
+        parts.run[i] = runs[i];
+        parts.base[i] = part_bytes[i];
+    }
+    if (next != cycle) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave_cycle_rgb8: parts must tile [0, cycle)");
+    if (!is_device_ptr(gathered) || !is_device_ptr(out))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_deinterleave_cycle_rgb8: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_deinterleave_cycle_rgb8(gathered, out, W, H, cycle, parts, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "deinterleave launch");
+    return mark_done(ctx);
+}
+
 rm_status rm_set_tile_order(rm_ctx *ctx, const uint32_t *order, int64_t n) {
     if (!ctx || n < 0 || (n > 0 && !order)) return RM_ERR_INVALID_ARGUMENT;
     RM_HIP(hipSetDevice(ctx->device));
@@ -1026,7 +1107,7 @@ rm_status rm_scene_eval(rm_ctx *ctx, const float *points, int64_t n, float *dist
     float *m = !material ? nullptr : dm ? material : reinterpret_cast<float *>(tmp + pb + db);
     hipError_t e = hipSuccess;
     if (!dp) e = hipMemcpyAsync(const_cast<float *>(p), points, pb, hipMemcpyHostToDevice, ctx->stream);
-    FrameConst F = frame_const(ctx, 1, 1, 1, 1, 0, 1);
+    FrameConst F = frame_const(ctx, 1, 1, RowPart{1, 0, 1}, 1);
     if (e == hipSuccess)
         e = ctx->scene == rm::SCENE_PLUGIN ? rmplugin::launch_eval(ctx->plugin, F, p, n, d, m, ctx->stream)
                                            : rm::launch_scene_eval(ctx->scene, F, p, n, d, m, ctx->stream);

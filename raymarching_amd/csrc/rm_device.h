@@ -43,7 +43,9 @@ struct FrameConst {
     float ry_c, ry_s, rx_c, rx_s;  // transformR(.., vec3(180, 2*u_time, 0)): rotationY(-2t), rotationX(-180);
                                    // rotationZ(-0) is the exact identity and is skipped
     int W, H;                      // target size (gl_TexCoord = ((x+.5)/W, (y+.5)/H))
-    int band, nshards, shard;      // row y is rendered iff (y / band) % nshards == shard
+    int cycle, offset, run;        // frame row y is rendered iff (y mod cycle) - offset lies in [0, run): row
+                                   // bands dealt round robin (band, nshards, shard) are run = band, cycle =
+                                   // band * nshards, offset = band * shard; weighted parts own longer runs
     int nrows;                     // packed rows rendered by this launch
     int row0;                      // first packed row of the shard this launch renders
     int max_steps;                 // MAX_MARCHING_STEPS (common.frag:15), run-time

@@ -11,6 +11,8 @@
 // (ray-steps); timing runs use COUNT=false.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rm_device.h"
 #include "rm_launch.h"
 
@@ -18,16 +20,17 @@ namespace rm {
 
 // gathered: nshards blocks of rows_per_shard packed rows (W elements each);
 // out: the W x H frame.  One thread per element (float4 or RGBA8 word).
+// Frame rows blockIdx.y, blockIdx.y + gridDim.y, ...: the shard / packed-row
+// arithmetic is wave-uniform (scalar), once per row.
 template <typename E>
 __global__ __launch_bounds__(256) void rm_deinterleave(const E* __restrict__ gathered, E* __restrict__ out, int W,
                                                          int H, int band, int nshards, int rows_per_shard) {
-    const size_t n = (size_t)W * H;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        int y = (int)(i / W), x = (int)(i - (size_t)y * W);
-        int gb = y / band, r = y - gb * band;
-        int shard = gb % nshards, lb = gb / nshards;
-        int j = lb * band + r;
-        out[i] = gathered[((size_t)shard * rows_per_shard + j) * W + x];
+    for (int y = blockIdx.y; y < H; y += gridDim.y) {
+        const int gb = y / band, r = y - gb * band;
+        const int shard = gb % nshards, lb = gb / nshards;
+        const E* src = gathered + ((size_t)shard * rows_per_shard + lb * band + r) * W;
+        E* dst = out + (size_t)y * W;
+        for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < W; x += gridDim.x * blockDim.x) dst[x] = src[x];
     }
 }
 
@@ -63,28 +66,58 @@ __global__ __launch_bounds__(256) void rm_pack_rgb8(const uint32_t* __restrict__
 }
 
 // gathered: nshards blocks of rows_per_shard packed rows of 3*W bytes; out:
-// the W x H RGBA8 frame (alpha 255).  vec (W % 4 == 0, aligned buffers): one
-// lane per 4 pixels (three 4-byte loads, one 16-byte store).
+// the W x H RGBA8 frame (alpha 255).  One workgroup row per frame row
+// (blockIdx.y = y: the shard / packed-row arithmetic is wave-uniform, scalar,
+// once per row); vec (W % 4 == 0, aligned buffers): one lane per 4 pixels
+// (three 4-byte loads, one 16-byte store).
 __global__ __launch_bounds__(256) void rm_deinterleave_rgb8(const uint8_t* __restrict__ gathered,
                                                               uint32_t* __restrict__ out, int W, int H, int band,
                                                               int nshards, int rows_per_shard, int vec) {
-    const size_t stride = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per_row = vec ? W / 4 : W;
-    const size_t n = (size_t)per_row * H;
-    for (size_t i = t0; i < n; i += stride) {
-        const int y = (int)(i / per_row), xg = (int)(i - (size_t)y * per_row);
-        const int gb = y / band, r = y - gb * band;
-        const int shard = gb % nshards, lb = gb / nshards;
-        const size_t src_row = ((size_t)shard * rows_per_shard + lb * band + r) * 3 * W;  // bytes
+    for (int y = blockIdx.y; y < H; y += gridDim.y) {
+    const int gb = y / band, r = y - gb * band;
+    const int shard = gb % nshards, lb = gb / nshards;
+    const uint8_t* src = gathered + ((size_t)shard * rows_per_shard + lb * band + r) * 3 * (size_t)W;
+    uint32_t* dst = out + (size_t)y * W;
+    for (int xg = blockIdx.x * blockDim.x + threadIdx.x; xg < per_row; xg += gridDim.x * blockDim.x) {
         if (vec) {
-            const uint32_t* s = reinterpret_cast<const uint32_t*>(gathered + src_row) + 3 * xg;
+            const uint32_t* s = reinterpret_cast<const uint32_t*>(src) + 3 * xg;
             const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
-            reinterpret_cast<uint4*>(out + (size_t)y * W)[xg] =
+            reinterpret_cast<uint4*>(dst)[xg] =
                 make_uint4((w0 & 0xFFFFFFu) | 0xFF000000u, (w0 >> 24) | ((w1 & 0xFFFFu) << 8) | 0xFF000000u,
                            (w1 >> 16) | ((w2 & 0xFFu) << 16) | 0xFF000000u, (w2 >> 8) | 0xFF000000u);
         } else {
-            const uint8_t* s = gathered + src_row + 3 * (size_t)xg;
-            out[(size_t)y * W + xg] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | 0xFF000000u;
+            const uint8_t* q = src + 3 * (size_t)xg;
+            dst[xg] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | 0xFF000000u;
+        }
+    }
+    }
+}
+
+// Frame rows of cyclic parts (rm_deinterleave_cycle_rgb8): part p owns the rows
+// y with (y mod cycle) - off[p] in [0, run[p]); its packed rows start at byte
+// base[p] of `gathered` (3 * W bytes each).  The parts partition [0, cycle).
+__global__ __launch_bounds__(256) void rm_deinterleave_cycle_rgb8(const uint8_t* __restrict__ gathered,
+                                                                    uint32_t* __restrict__ out, int W, int H,
+                                                                    int cycle, CycleParts parts, int vec) {
+    const int per_row = vec ? W / 4 : W;
+    for (int y = blockIdx.y; y < H; y += gridDim.y) {
+        const int c = y / cycle, m = y - c * cycle;
+        int p = 0;
+        while (p + 1 < parts.n && parts.off[p + 1] <= m) p++;  // (wave-uniform)
+        const uint8_t* src = gathered + parts.base[p] + ((size_t)c * parts.run[p] + (m - parts.off[p])) * 3 * (size_t)W;
+        uint32_t* dst = out + (size_t)y * W;
+        for (int xg = blockIdx.x * blockDim.x + threadIdx.x; xg < per_row; xg += gridDim.x * blockDim.x) {
+            if (vec) {
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(src) + 3 * xg;
+                const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
+                reinterpret_cast<uint4*>(dst)[xg] =
+                    make_uint4((w0 & 0xFFFFFFu) | 0xFF000000u, (w0 >> 24) | ((w1 & 0xFFFFu) << 8) | 0xFF000000u,
+                               (w1 >> 16) | ((w2 & 0xFFu) << 16) | 0xFF000000u, (w2 >> 8) | 0xFF000000u);
+            } else {
+                const uint8_t* q = src + 3 * (size_t)xg;
+                dst[xg] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | 0xFF000000u;
+            }
         }
     }
 }
@@ -216,11 +249,10 @@ hipError_t launch_scene_eval(int scene, const FrameConst& F, const float* pts, l
 template <typename E>
 static hipError_t deinterleave_t(const E* gathered, E* out, int W, int H, int band, int nshards, int rows_per_shard,
                                  hipStream_t s) {
-    size_t n = (size_t)W * H;
-    if (!n) return hipSuccess;
-    unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
-    hipLaunchKernelGGL(rm_deinterleave<E>, dim3(blocks), dim3(256), 0, s, gathered, out, W, H, band, nshards,
-                       rows_per_shard);
+    if (W <= 0 || H <= 0) return hipSuccess;
+    const unsigned bx = (unsigned)std::min((W + 255) / 256, 64);
+    hipLaunchKernelGGL(rm_deinterleave<E>, dim3(bx, (unsigned)std::min(H, 65535)), dim3(256), 0, s, gathered, out, W, H,
+                       band, nshards, rows_per_shard);
     return hipGetLastError();
 }
 
@@ -250,15 +282,27 @@ hipError_t launch_pack_rgb8(const uint32_t* in, uint8_t* out, size_t n, hipStrea
     return hipGetLastError();
 }
 
+hipError_t launch_deinterleave_cycle_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int cycle,
+                                          const CycleParts& parts, hipStream_t s) {
+    if (W <= 0 || H <= 0) return hipSuccess;
+    int vec = (W % 4 == 0) && ((uintptr_t)gathered % 4 == 0) && ((uintptr_t)out % 16 == 0);
+    for (int p = 0; p < parts.n; p++) vec = vec && parts.base[p] % 4 == 0;
+    const int per_row = vec ? W / 4 : W;
+    const unsigned bx = (unsigned)std::min((per_row + 255) / 256, 64);
+    hipLaunchKernelGGL(rm_deinterleave_cycle_rgb8, dim3(bx, (unsigned)std::min(H, 65535)), dim3(256), 0, s, gathered,
+                       out, W, H, cycle, parts, vec);
+    return hipGetLastError();
+}
+
 hipError_t launch_deinterleave_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
                                     int rows_per_shard, hipStream_t s) {
     const size_t n = (size_t)W * H;
     if (!n) return hipSuccess;
     const int vec = (W % 4 == 0) && ((uintptr_t)gathered % 4 == 0) && ((uintptr_t)out % 16 == 0);
-    const size_t work = vec ? n / 4 : n;
-    unsigned blocks = (unsigned)((work + 255) / 256 < 8192 ? (work + 255) / 256 : 8192);
-    hipLaunchKernelGGL(rm_deinterleave_rgb8, dim3(blocks), dim3(256), 0, s, gathered, out, W, H, band, nshards,
-                       rows_per_shard, vec);
+    const int per_row = vec ? W / 4 : W;
+    const unsigned bx = (unsigned)std::min((per_row + 255) / 256, 64);
+    hipLaunchKernelGGL(rm_deinterleave_rgb8, dim3(bx, (unsigned)std::min(H, 65535)), dim3(256), 0, s, gathered, out,
+                       W, H, band, nshards, rows_per_shard, vec);
     return hipGetLastError();
 }
 

@@ -33,6 +33,16 @@ hipError_t launch_pack_rgba8(const float4* in, uint32_t* out, size_t n, hipStrea
 hipError_t launch_pack_rgb8(const uint32_t* in, uint8_t* out, size_t n, hipStream_t s);
 hipError_t launch_deinterleave_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int band, int nshards,
                                     int rows_per_shard, hipStream_t s);
+// cyclic parts of a frame (rm_deinterleave_cycle_rgb8): part p owns the rows y
+// with (y mod cycle) - off[p] in [0, run[p]), its packed RGB8 rows from byte base[p]
+constexpr int kMaxCycleParts = 64;
+struct CycleParts {
+    int n;
+    int off[kMaxCycleParts], run[kMaxCycleParts];
+    long long base[kMaxCycleParts];
+};
+hipError_t launch_deinterleave_cycle_rgb8(const uint8_t* gathered, uint32_t* out, int W, int H, int cycle,
+                                          const CycleParts& parts, hipStream_t s);
 // the next launch's tile order (costliest first) from the tile durations
 // (hist: 256 counts + 256 cursors, zero on entry); clears `next` (512 words)
 // for the following launch

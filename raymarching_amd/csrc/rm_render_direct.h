@@ -803,8 +803,8 @@ __device__ __forceinline__ void store_pixel(const FrameConst& F, OUT* __restrict
 
 // local packed row j of this shard -> frame row y
 __device__ __forceinline__ int shard_row(const FrameConst& F, int j) {
-    int b = j / F.band, r = j - b * F.band;
-    return (b * F.nshards + F.shard) * F.band + r;
+    int c = j / F.run, r = j - c * F.run;
+    return c * F.cycle + F.offset + r;
 }
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {

@@ -18,21 +18,51 @@ from dataclasses import dataclass
 
 @dataclass(frozen=True)
 class ShardPlan:
+    """Which frame rows each shard renders.  Every shard owns one run of
+    consecutive rows in each cycle of ``cycle`` rows: shard s owns row y iff
+    ``(y mod cycle) - offsets[s]`` lies in ``[0, runs[s])``.  ``runs`` None is
+    round-robin bands (every run = ``band``); explicit ``runs`` weight the
+    shards (bench.py's balanced split gives the root, which also receives
+    every other shard's rows, a longer run)."""
     W: int
     H: int
     band: int
     nshards: int
+    runs: tuple | None = None
+
+    def __post_init__(self):
+        if self.runs is not None and (len(self.runs) != self.nshards or min(self.runs) < 1):
+            raise ValueError(f"runs must hold {self.nshards} positive row counts, got {self.runs}")
+
+    @property
+    def weighted(self) -> bool:
+        return self.runs is not None
+
+    @property
+    def part_runs(self) -> tuple:
+        return tuple(self.runs) if self.runs is not None else (self.band,) * self.nshards
+
+    @property
+    def cycle(self) -> int:
+        return sum(self.part_runs)
+
+    @property
+    def offsets(self) -> tuple:
+        o, acc = [], 0
+        for r in self.part_runs:
+            o.append(acc)
+            acc += r
+        return tuple(o)
 
     def rows(self, shard: int) -> list[int]:
         """Frame rows of `shard`, in packed (increasing) order."""
-        return [y for y in range(self.H) if (y // self.band) % self.nshards == shard]
+        c, o, r = self.cycle, self.offsets[shard], self.part_runs[shard]
+        return [y for y in range(self.H) if 0 <= y % c - o < r]
 
     def count(self, shard: int) -> int:
-        nb = -(-self.H // self.band)
-        n = 0
-        for b in range(shard, nb, self.nshards):
-            n += self.H - b * self.band if b == nb - 1 else self.band
-        return n
+        c, o, r = self.cycle, self.offsets[shard], self.part_runs[shard]
+        full, rest = divmod(self.H, c)
+        return full * r + min(max(rest - o, 0), r)
 
     @property
     def rows_per_shard(self) -> int:
@@ -41,14 +71,28 @@ class ShardPlan:
 
     def slot_of_row(self, y: int) -> tuple[int, int]:
         """(shard, packed row) holding frame row y."""
-        gb, r = divmod(y, self.band)
-        shard, lb = gb % self.nshards, gb // self.nshards
-        return shard, lb * self.band + r
+        cyc, m = divmod(y, self.cycle)
+        offs, runs = self.offsets, self.part_runs
+        s = max(i for i in range(self.nshards) if offs[i] <= m)
+        return s, cyc * runs[s] + m - offs[s]
 
     def gathered_index(self):
         """Flat index into the [nshards * rows_per_shard] gathered rows for every frame row."""
         rps = self.rows_per_shard
         return [s * rps + j for s, j in (self.slot_of_row(y) for y in range(self.H))]
+
+    def part_bases(self) -> list[int]:
+        """First row of each shard in the unpadded gather (shards back to back)."""
+        b, acc = [], 0
+        for s in range(self.nshards):
+            b.append(acc)
+            acc += self.count(s)
+        return b
+
+    def packed_index(self):
+        """Flat index into the unpadded gathered rows for every frame row."""
+        base = self.part_bases()
+        return [base[s] + j for s, j in (self.slot_of_row(y) for y in range(self.H))]
 
 
 def gather_to_root(local, plan: ShardPlan, rank: int, group=None, out=None):
@@ -76,6 +120,36 @@ def gather_to_root(local, plan: ShardPlan, rank: int, group=None, out=None):
             out.copy_(dst)
         return out
     dist.gather(src, gather_list=None, dst=0, group=group)
+    return None
+
+
+def gather_parts_to_root(local, plan: ShardPlan, rank: int, group=None, out=None):
+    """Gather each rank's packed rows, unpadded, into the [sum of counts, ...]
+    tensor `out` on rank 0 (shards back to back, ShardPlan.part_bases), with
+    point-to-point sends: the shards of a weighted plan differ in size.  Rank
+    0's own rows must already be in place (its render writes there).  gloo
+    (host memory) stages device buffers; the CPU tests use it."""
+    import torch
+    import torch.distributed as dist
+
+    staged = local.is_cuda and dist.get_backend(group) == "gloo"
+    if rank == 0:
+        base = plan.part_bases()
+        for r in range(1, plan.nshards):
+            n = plan.count(r)
+            if n == 0:
+                continue
+            dst = out[base[r]: base[r] + n]
+            buf = torch.empty(dst.shape, dtype=dst.dtype) if staged else dst
+            dist.recv(buf, src=r, group=group)
+            if staged:
+                dst.copy_(buf)
+        return out
+    n = plan.count(rank)
+    if local.shape[0] < n:
+        raise ValueError(f"local rows {local.shape[0]} < this shard's {n}")
+    if n:
+        dist.send(local[:n].cpu() if staged else local[:n].contiguous(), dst=0, group=group)
     return None
 
 
@@ -107,7 +181,7 @@ class DistributedFrame:
     """
 
     def __init__(self, renderer, W, H, band, rank, world, fmt="rgba8", group=None, chunks=1, wire="auto",
-                 streams=None):
+                 streams=None, runs=None):
         import torch
 
         self.r, self.rank, self.world, self.fmt, self.group = renderer, rank, world, fmt, group
@@ -119,7 +193,13 @@ class DistributedFrame:
             raise ValueError(f"wire {wire!r} does not carry {fmt!r} frames")
         self.wire = wire
         # one shard: the packed rows are the frame rows (no de-interleave needed)
-        self.plan = ShardPlan(W, H, band if world > 1 else H, world)
+        if runs is not None and world > 1:
+            # weighted parts: unpadded point-to-point gather of RGB8 rows
+            if wire != "rgb8":
+                raise ValueError("weighted row parts (runs) need the RGB8 wire (fmt='rgba8')")
+            self.plan = ShardPlan(W, H, band, world, tuple(int(x) for x in runs))
+        else:
+            self.plan = ShardPlan(W, H, band if world > 1 else H, world)
         dev = torch.device(f"cuda:{renderer.device}")
         if streams is None:
             streams = 2 if self._pipelined() else 1
@@ -129,11 +209,28 @@ class DistributedFrame:
         rps = self.plan.rows_per_shard
         self.nmine = self.plan.count(rank)
         chunks = max(1, min(int(chunks), rps))
-        self.cuts = [round(c * rps / chunks) for c in range(chunks + 1)]
+        if self.plan.weighted:
+            # every shard cuts its own rows into the same number of chunks
+            self.all_cuts = [[round(c * self.plan.count(q) / chunks) for c in range(chunks + 1)]
+                             for q in range(world)]
+            self.cuts = self.all_cuts[rank]
+        else:
+            self.cuts = [round(c * rps / chunks) for c in range(chunks + 1)]
         nbuf = 2 if world > 1 or streams > 1 else 1
         shape = (rps, W) if fmt == "rgba8" else (rps, W, 4)
         dtype = torch.int32 if fmt == "rgba8" else torch.float32
-        if self.wire == "rgb8":
+        if self.plan.weighted:
+            # shards back to back in the root's gather buffer; the root packs its
+            # own rows straight into the head of it
+            n = self.nmine
+            self.locals = [torch.empty((n, W), dtype=dtype, device=dev) for _ in range(nbuf)]
+            if rank == 0:
+                self.gathered = [torch.empty((H, 3 * W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+                self.wires = [g[:n] for g in self.gathered]
+            else:
+                self.gathered = None
+                self.wires = [torch.empty((n, 3 * W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        elif self.wire == "rgb8":
             # render into a local RGBA8 band, pack each chunk into the slot being gathered
             self.locals = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nbuf)]
             self.wires = [torch.empty((rps, 3 * W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
@@ -141,9 +238,10 @@ class DistributedFrame:
             # the render kernel writes straight into the slot being gathered
             self.locals = None
             self.wires = [torch.empty(shape, dtype=dtype, device=dev) for _ in range(nbuf)]
-        wire = self.wires[0]
-        self.gathered = ([torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev) for _ in range(2)]
-                         if rank == 0 and world > 1 else None)
+        if not self.plan.weighted:
+            wire = self.wires[0]
+            self.gathered = ([torch.empty((world,) + tuple(wire.shape), dtype=wire.dtype, device=dev)
+                              for _ in range(2)] if rank == 0 and world > 1 else None)
         if world == 1:
             self.frames = self.wires if self.locals is None else self.locals
         elif rank == 0:
@@ -159,37 +257,74 @@ class DistributedFrame:
         import torch.distributed as dist
         return self.world > 1 and dist.get_backend(self.group) != "gloo"
 
-    def _render_rows(self, j0, j1, slot, events=None):
+    def _render_into(self, dst, j0, j1, stats=False):
+        """Packed rows [j0, j1) of this rank's part into dst[j0:j1]."""
         p = self.plan
+        if p.weighted:
+            return self.r.render_cycle_rows(p.W, p.H, p.cycle, p.offsets[self.rank], p.part_runs[self.rank], j0,
+                                            j1 - j0, dst[j0:j1], stats=stats)
+        return self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, dst[j0:j1], stats=stats)
+
+    def _render_rows(self, j0, j1, slot, events=None):
         j1 = min(j1, self.nmine)
         if j1 <= j0:
             return
         dst = self.wires[slot] if self.locals is None else self.locals[slot]
         if events is not None:
             events[0].record()
-        self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, dst[j0:j1])
+        self._render_into(dst, j0, j1)
         if events is not None:
             events[1].record()
         if self.locals is not None:
             self.r.pack_rgb8(self.locals[slot][j0:j1], out=self.wires[slot][j0:j1])
 
-    def _gather_async(self, slot, j0, j1):
+    def _gather_async(self, slot, c):
+        """Start chunk c's gather (c None: every row); returns the works."""
         import torch.distributed as dist
+        p = self.plan
+        if p.weighted:  # point-to-point: the parts differ in size
+            ops = []
+            if self.rank == 0:
+                base = p.part_bases()
+                for q in range(1, self.world):
+                    cq = self.all_cuts[q]
+                    j0, j1 = (0, p.count(q)) if c is None else (cq[c], cq[c + 1])
+                    if j1 > j0:
+                        ops.append(dist.P2POp(dist.irecv, self.gathered[slot][base[q] + j0: base[q] + j1], q,
+                                              group=self.group))
+            else:
+                j0, j1 = (0, self.nmine) if c is None else (self.cuts[c], self.cuts[c + 1])
+                if j1 > j0:
+                    ops.append(dist.P2POp(dist.isend, self.wires[slot][j0:j1], 0, group=self.group))
+            return dist.batch_isend_irecv(ops) if ops else []
+        j0, j1 = (0, p.rows_per_shard) if c is None else (self.cuts[c], self.cuts[c + 1])
         g = self.gathered[slot] if self.rank == 0 else None
         glist = [g[r, j0:j1] for r in range(self.world)] if self.rank == 0 else None
-        return dist.gather(self.wires[slot][j0:j1], gather_list=glist, dst=0, group=self.group, async_op=True)
+        return [dist.gather(self.wires[slot][j0:j1], gather_list=glist, dst=0, group=self.group, async_op=True)]
+
+    def _gather_blocking(self, slot):
+        """The host-staged gather (gloo), completed inside the call."""
+        if self.plan.weighted:
+            gather_parts_to_root(self.wires[slot], self.plan, self.rank, group=self.group,
+                                 out=self.gathered[slot] if self.rank == 0 else None)
+        else:
+            gather_to_root(self.wires[slot], self.plan, self.rank, group=self.group,
+                           out=self.gathered[slot] if self.rank == 0 else None)
 
     def _deinterleave(self, slot):
         p = self.plan
-        self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered[slot],
-                            out=self.frames[slot])
+        if p.weighted:
+            self.r.deinterleave_cycle_rgb8(p.W, p.H, p.cycle, list(p.offsets), list(p.part_runs),
+                                           [b * 3 * p.W for b in p.part_bases()], self.gathered[slot],
+                                           out=self.frames[slot])
+        else:
+            self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered[slot],
+                                out=self.frames[slot])
 
     def render_local(self, stats=False):
         """This rank's rows only, into slot 0 (no gather); stats: one synchronous launch."""
-        p = self.plan
         dst = self.wires[0] if self.locals is None else self.locals[0]
-        return self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, 0, self.nmine, dst[: self.nmine],
-                                  stats=stats)
+        return self._render_into(dst, 0, self.nmine, stats=stats)
 
     def submit(self, events=None):
         """Enqueue one frame.  With N > 1 its gather stays in flight until the
@@ -207,10 +342,9 @@ class DistributedFrame:
             for c in range(nch):
                 self._render_rows(self.cuts[c], self.cuts[c + 1], slot, None if events is None else events[c])
                 if self._pipelined():
-                    works.append(self._gather_async(slot, self.cuts[c], self.cuts[c + 1]))
+                    works.extend(self._gather_async(slot, c))
             if self.world > 1 and not self._pipelined():  # gloo: one host-staged gather, completed here
-                gather_to_root(self.wires[slot], self.plan, self.rank, group=self.group,
-                               out=self.gathered[slot] if self.rank == 0 else None)
+                self._gather_blocking(slot)
                 works = None
         self.r.set_stream(self.streams[0])
         if self.world == 1:
@@ -274,8 +408,7 @@ class DistributedFrame:
         with torch.cuda.stream(st):
             ev[0].record(st)
             if self.nmine:
-                dst = self.wires[slot] if self.locals is None else self.locals[slot]
-                self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, 0, self.nmine, dst[: self.nmine])
+                self._render_into(self.wires[slot] if self.locals is None else self.locals[slot], 0, self.nmine)
             ev[1].record(st)
             if self.locals is not None and self.nmine:
                 self.r.pack_rgb8(self.locals[slot][: self.nmine], out=self.wires[slot][: self.nmine])
@@ -289,14 +422,14 @@ class DistributedFrame:
         if self._pipelined():
             with torch.cuda.stream(st):
                 ev[3].record(st)
-                self._gather_async(slot, 0, p.rows_per_shard).wait()  # st waits for the gather
+                for w in self._gather_async(slot, None):
+                    w.wait()  # st waits for the gather
                 ev[4].record(st)
             torch.cuda.synchronize(dev)
             out["gather_ms"] = ev[3].elapsed_time(ev[4])
         else:  # gloo: host-staged, completes inside the call
             t0 = time.perf_counter()
-            gather_to_root(self.wires[slot], p, self.rank, group=self.group,
-                           out=self.gathered[slot] if self.rank == 0 else None)
+            self._gather_blocking(slot)
             torch.cuda.synchronize(dev)
             out["gather_ms"] = (time.perf_counter() - t0) * 1e3
         if self.rank == 0:

@@ -663,13 +663,16 @@ class _FakeWork:
             torch.cuda.current_stream().wait_event(self.ev)
 
 
-def test_pipelined_two_stream_frames_in_one_process(R, torch_cuda):
+@pytest.mark.parametrize("runs", [None, (13, 8), (3, 8)])
+def test_pipelined_two_stream_frames_in_one_process(R, torch_cuda, runs):
     """DistributedFrame's RCCL path (pipelined gathers, two HIP streams, per-slot
     buffers) for two ranks living in one process, with the gather replaced by
     device copies on a side stream that honour the same stream semantics as
     ProcessGroupNCCL (wait on the caller's stream, work.wait() makes the
     caller's stream wait).  Every frame of a pose sequence must equal the
-    one-rank rm_render_rgba8 frame."""
+    one-rank rm_render_rgba8 frame.  runs: round-robin bands (None) or weighted
+    cyclic parts (rank 0 renders a longer / shorter run of every cycle; the
+    unpadded point-to-point gather and rm_deinterleave_cycle_rgb8)."""
     torch = torch_cuda
     from raymarching_amd.frame import DistributedFrame
     W, H, band = 96, 70, 8
@@ -677,21 +680,28 @@ def test_pipelined_two_stream_frames_in_one_process(R, torch_cuda):
     sent = {}
 
     def fake_gather(fr):
-        def gather(slot, j0, j1):
+        def gather(slot, c):
+            cuts = fr.cuts
+            j0, j1 = (0, fr.nmine if fr.plan.weighted else fr.plan.rows_per_shard) if c is None else (cuts[c], cuts[c + 1])
             ev = torch.cuda.Event()
             ev.record()  # the caller's (frame) stream
             if fr.rank == 1:
-                sent[(fr.k, j0)] = (fr.wires[slot][j0:j1], ev)
-                return _FakeWork()
-            src1, ev1 = sent.pop((fr.k, j0))
+                sent[(fr.k, c)] = (fr.wires[slot][j0:j1], ev)
+                return [_FakeWork()]
+            src1, ev1 = sent.pop((fr.k, c))
             side.wait_event(ev)
             side.wait_event(ev1)
             with torch.cuda.stream(side):
-                fr.gathered[slot][0, j0:j1].copy_(fr.wires[slot][j0:j1])
-                fr.gathered[slot][1, j0:j1].copy_(src1)
+                if fr.plan.weighted:  # rank 0's rows are in place; rank 1's chunk c lands after them
+                    b = fr.plan.part_bases()[1]
+                    k0, k1 = (0, fr.plan.count(1)) if c is None else (fr.all_cuts[1][c], fr.all_cuts[1][c + 1])
+                    fr.gathered[slot][b + k0: b + k1].copy_(src1)
+                else:
+                    fr.gathered[slot][0, j0:j1].copy_(fr.wires[slot][j0:j1])
+                    fr.gathered[slot][1, j0:j1].copy_(src1)
             done = torch.cuda.Event()
             done.record(side)
-            return _FakeWork(done)
+            return [_FakeWork(done)]
         return gather
 
     r1 = rm.Renderer(0)
@@ -699,7 +709,7 @@ def test_pipelined_two_stream_frames_in_one_process(R, torch_cuda):
     for rank, rr in ((0, R), (1, r1)):
         f = DistributedFrame.__new__(DistributedFrame)
         f._pipelined = lambda: True  # as with the "nccl" backend
-        DistributedFrame.__init__(f, rr, W, H, band, rank, 2, fmt="rgba8", chunks=2)
+        DistributedFrame.__init__(f, rr, W, H, band, rank, 2, fmt="rgba8", chunks=2, runs=runs)
         f._gather_async = fake_gather(f)
         frs.append(f)
     assert len(frs[0].streams) == 2 and frs[0].wire == "rgb8"
@@ -853,3 +863,40 @@ def test_settled_soft_shadows_keep_pixels(R, torch_cuda, scene, pose):
     # both skip the shadow marches of points facing away from the light)
     frac_hip, frac_ref = st["skipped"] / st["evals"], o_skip / st["evals"]
     assert abs(frac_hip - frac_ref) <= 0.02, (frac_hip, frac_ref, st, o)
+
+
+@pytest.mark.parametrize("W,H,runs", [(96, 70, (13, 8)), (97, 61, (1, 5, 2)), (128, 300, (40, 16, 16, 16))])
+def test_weighted_cycle_parts_rebuild_frame(R, torch_cuda, W, H, runs):
+    """Weighted cyclic row parts (bench.py --balance auto): each part rendered
+    with rm_render_cycle_rows_rgba8 (and the float4 form), packed to the RGB8
+    wire back to back, and rm_deinterleave_cycle_rgb8 gives the one-launch
+    rm_render_rgba8 frame bit for bit; parts that do not tile the cycle are
+    refused."""
+    torch = torch_cuda
+    from raymarching_amd.frame import ShardPlan
+    setup(R, "T", POSES["P1"], 128)
+    R.set_params(count_evals=0)
+    ref = R.render_rgba8(W, H)
+    ref4 = R.render(W, H)
+    plan = ShardPlan(W, H, runs[-1], len(runs), runs)
+    gathered = torch.empty((H, 3 * W), dtype=torch.uint8, device="cuda")
+    base = plan.part_bases()
+    for s in range(len(runs)):
+        n = plan.count(s)
+        loc = torch.empty((n, W), dtype=torch.int32, device="cuda")
+        # two calls over a split of the packed rows, as chunked frames do
+        h = n // 2
+        R.render_cycle_rows(W, H, plan.cycle, plan.offsets[s], runs[s], 0, h, loc)
+        R.render_cycle_rows(W, H, plan.cycle, plan.offsets[s], runs[s], h, n - h, loc[h:])
+        R.pack_rgb8(loc, out=gathered[base[s]: base[s] + n])
+        f4 = torch.empty((n, W, 4), dtype=torch.float32, device="cuda")
+        R.render_cycle_rows(W, H, plan.cycle, plan.offsets[s], runs[s], 0, n, f4)
+        assert torch.equal(f4, ref4[plan.rows(s)])
+    frame = R.deinterleave_cycle_rgb8(W, H, plan.cycle, list(plan.offsets), list(runs),
+                                      [b * 3 * W for b in base], gathered)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, ref)
+    with pytest.raises(rm.RmError):  # a gap in [0, cycle)
+        R.deinterleave_cycle_rgb8(W, H, plan.cycle + 1, list(plan.offsets), list(runs), [0] * len(runs), gathered)
+    with pytest.raises(rm.RmError):
+        R.render_cycle_rows(W, H, 4, 3, 2, 0, 1, frame[:1])

@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""N-GPU frame model from one GPU: every rank's share of an
+N-way row split rendered on this GPU as that rank would render it in the
+pipelined bench (two HIP streams, RGBA8 kernel + RGB8 pack per frame, frames
+back to back; no gather), the root's de-interleave of the whole frame, and
+the wire bytes each rank sends.  The projected frame time at N is
+
+    max( max over ranks of the rank's per-frame compute (+ de-interleave on the root),
+         the largest non-root wire / the assumed per-link xGMI rate )
+
+(each non-root rank's rows cross their own link, concurrently, while the next
+frame renders).  The link rate is an assumption (--link-gbs), printed with
+the result; the driver's 8-GPU run measures the real gather (bench.py
+gather_ms).  Both the even split (bands of 16) and bench.py's balanced split
+(balanced_runs, sized with the same link assumption) are modelled.
+
+Usage: scale_model.py [--config C3|C5] [--ns 1,2,4,8] [--frames 24] [--link-gbs 64]
+One JSON line per (N, split)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+CONFIGS = {  # scene, W, H, max steps, pose
+    "C3": ("T", 4096, 4096, 256, "P0"),
+    "C5": ("O", 8192, 8192, 512, "P0"),
+    "C3P1": ("T", 4096, 4096, 256, "P1"),
+}
+
+
+def per_frame_ms(r, torch, plan, rank, frames):
+    """Rank's pipelined per-frame compute: render (RGBA8) + pack (RGB8) on two
+    alternating streams, `frames` frames, wall time / frames."""
+    p = plan
+    n = p.count(rank)
+    if n == 0:
+        return 0.0, 0.0
+    W = p.W
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    loc = [torch.empty((n, W), dtype=torch.int32, device="cuda") for _ in streams]
+    wire = [torch.empty((n, 3 * W), dtype=torch.uint8, device="cuda") for _ in streams]
+
+    def one(i):
+        st = streams[i % 2]
+        with torch.cuda.stream(st):
+            r.set_stream(st)
+            r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[i % 2])
+            r.pack_rgb8(loc[i % 2], out=wire[i % 2])
+        r.set_stream(streams[0])
+
+    t_end = time.time() + 0.3
+    i = 0
+    while time.time() < t_end or i < 16:  # clock ramp + adaptive order settled on both streams
+        one(i)
+        i += 1
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(frames):
+        one(j)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / frames * 1e3
+    # single synchronous launch (the bench's kernel_ms) for the record
+    r.set_stream(streams[0])
+    ks = sorted(r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[0],
+                                    stats=True)[1]["kernel_ms"] for _ in range(7))
+    return ms, ks[len(ks) // 2]
+
+
+def deinterleave_ms(r, torch, plan):
+    W, H = plan.W, plan.H
+    g = torch.randint(0, 255, (H, 3 * W), dtype=torch.uint8, device="cuda")
+    out = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    bases = [b * 3 * W for b in plan.part_bases()]
+    args = (W, H, plan.cycle, list(plan.offsets), list(plan.part_runs), bases, g)
+    for _ in range(20):
+        r.deinterleave_cycle_rgb8(*args, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        r.deinterleave_cycle_rgb8(*args, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 50
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
+    ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--frames", type=int, default=24)
+    ap.add_argument("--band", type=int, default=16)
+    ap.add_argument("--link-gbs", type=float, default=64.0,
+                    help="assumed xGMI rate of one link, one direction, as RCCL point-to-point achieves it (GB/s)")
+    args = ap.parse_args()
+    import torch
+
+    import raymarching_amd as rm
+    from bench import balanced_runs
+    from raymarching_amd.frame import ShardPlan
+
+    scene, W, H, steps, pose = CONFIGS[args.config]
+    r = rm.Renderer(0)
+    r.load_scene(rm.SCENE_FILES[scene])
+    r.set_uniform("u_resolution", W, H)
+    pz = rm.POSES[pose]
+    r.set_pose(pz["pos"], pz["mouse"], pz["time"])
+    r.set_params(max_steps=steps, shadow_max_steps=0, count_evals=0, schedule=1)
+    link_bpms = args.link_gbs * 1e6  # bytes per ms
+    for N in [int(x) for x in args.ns.split(",")]:
+        even = ShardPlan(W, H, args.band if N > 1 else H, N, None if N > 1 else (H,))
+        per = [per_frame_ms(r, torch, even, q, args.frames) for q in range(N)]
+        d = deinterleave_ms(r, torch, even) if N > 1 else 0.0
+        rows = {"even": (even, per, d)}
+        if N > 1:
+            ex = {"render_ms": [x[0] for x in per], "gather_ms": max(even.count(q) for q in range(1, N)) * 3 * W
+                  / link_bpms, "deinterleave_ms": d}
+            runs, model = balanced_runs(N, args.band, H, ex)
+            bal = ShardPlan(W, H, args.band, N, tuple(runs))
+            perb = [per_frame_ms(r, torch, bal, q, args.frames) for q in range(N)]
+            rows["balanced"] = (bal, perb, deinterleave_ms(r, torch, bal))
+        for name, (plan, pr, dms) in rows.items():
+            wire = [plan.count(q) * 3 * W for q in range(N)]
+            link = max(wire[1:], default=0) / link_bpms
+            compute = [pr[0][0] + dms] + [x[0] for x in pr[1:]]
+            frame = max(max(compute), link)
+            print(json.dumps({
+                "config": args.config, "N": N, "split": name, "runs": list(plan.part_runs),
+                "per_rank_frame_ms": [round(x[0], 4) for x in pr],
+                "per_rank_kernel_ms": [round(x[1], 4) for x in pr],
+                "deinterleave_ms": round(dms, 4), "wire_bytes": wire, "link_gbs_assumed": args.link_gbs,
+                "link_ms": round(link, 4), "projected_frame_ms": round(frame, 4),
+                "bound": "link" if link >= max(compute) else ("root" if compute[0] >= max(compute[1:], default=0)
+                                                              else "rank"),
+            }), flush=True)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
