@@ -153,6 +153,53 @@ def gather_parts_to_root(local, plan: ShardPlan, rank: int, group=None, out=None
     return None
 
 
+def _runs_concurrently(a, b, cycles=400_000):
+    """True if kernels on streams a and b overlap: a spin kernel on each, the
+    pair timed on the host.  Two streams that share a hardware queue run one
+    after the other."""
+    import time
+
+    import torch
+    spin = getattr(torch.cuda, "_sleep", None)
+    if spin is None:
+        return True
+    best = float("inf"), float("inf")
+    for _ in range(2):
+        ts = []
+        for streams in ((a,), (a, b)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for st in streams:
+                with torch.cuda.stream(st):
+                    spin(cycles)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        best = min(best[0], ts[0]), min(best[1], ts[1])
+    return best[1] < 1.5 * best[0]
+
+
+def concurrent_streams(dev, n, tries=12):
+    """n HIP streams of `dev` whose kernels run concurrently.  HIP maps a
+    process's streams onto at most GPU_MAX_HW_QUEUES hardware queues (4 on
+    MI355X nodes by default) and two streams on one queue serialize; which
+    streams share depends on how many the process (PyTorch's pool, RCCL) made
+    before, so the pairs are probed (tools/queue_probe.py: 1 in 4 to 1 in 8
+    pool streams shared a queue with the default stream).  Falls back to the
+    last candidates if none of `tries` qualify."""
+    import torch
+    with torch.cuda.device(dev):
+        chosen = [torch.cuda.Stream(dev)]
+        for _ in range(tries):
+            if len(chosen) == n:
+                break
+            c = torch.cuda.Stream(dev)
+            if all(_runs_concurrently(c, s) for s in chosen):
+                chosen.append(c)
+        while len(chosen) < n:
+            chosen.append(torch.cuda.Stream(dev))
+    return chosen
+
+
 class DistributedFrame:
     """One rank's share of a row-sharded frame on its GPU.
 
@@ -205,7 +252,13 @@ class DistributedFrame:
             streams = 2 if self._pipelined() else 1
         if streams not in (1, 2):
             raise ValueError("streams must be 1 or 2")
-        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(streams - 1)]
+        # one stream: the caller's; two: a probed pair that does not share a
+        # hardware queue (on one queue the frames would not overlap)
+        self.caller = torch.cuda.current_stream(dev)
+        self.streams = [self.caller] if streams == 1 else concurrent_streams(dev, streams)
+        if streams > 1:  # the frame streams start after the caller's work so far
+            for st in self.streams:
+                st.wait_stream(self.caller)
         rps = self.plan.rows_per_shard
         self.nmine = self.plan.count(rank)
         chunks = max(1, min(int(chunks), rps))
@@ -322,9 +375,21 @@ class DistributedFrame:
                                 out=self.frames[slot])
 
     def render_local(self, stats=False):
-        """This rank's rows only, into slot 0 (no gather); stats: one synchronous launch."""
+        """This rank's rows only, into slot 0 (no gather), on the first frame
+        stream (whose adaptive tile order the frames use); stats: one
+        synchronous launch.  Ordered before later work on the caller's stream."""
+        import torch
         dst = self.wires[0] if self.locals is None else self.locals[0]
-        return self._render_into(dst, 0, self.nmine, stats=stats)
+        st = self.streams[0]
+        with torch.cuda.stream(st):
+            self.r.set_stream(st)
+            try:
+                res = self._render_into(dst, 0, self.nmine, stats=stats)
+            finally:
+                self.r.set_stream(self.caller)
+        if st is not self.caller:
+            self.caller.wait_stream(st)
+        return res
 
     def submit(self, events=None):
         """Enqueue one frame.  With N > 1 its gather stays in flight until the
@@ -346,7 +411,7 @@ class DistributedFrame:
             if self.world > 1 and not self._pipelined():  # gloo: one host-staged gather, completed here
                 self._gather_blocking(slot)
                 works = None
-        self.r.set_stream(self.streams[0])
+        self.r.set_stream(self.caller)
         if self.world == 1:
             self.frame = self.frames[slot]
         prev, self.pending = self.pending, (slot, st, works) if self.world > 1 else None
@@ -365,7 +430,7 @@ class DistributedFrame:
             if self.rank == 0:
                 self._deinterleave(slot)
                 self.frame = self.frames[slot]
-        self.r.set_stream(self.streams[0])
+        self.r.set_stream(self.caller)
 
     def flush(self):
         """Finish the frame in flight (rank 0: its de-interleaved frame is in
@@ -379,6 +444,8 @@ class DistributedFrame:
             ev = torch.cuda.Event()
             ev.record(st)
             self.streams[0].wait_event(ev)
+        if self.streams[0] is not self.caller:  # ... and the caller's stream after them
+            self.caller.wait_stream(self.streams[0])
         return self.frame
 
     def render(self, events=None):
@@ -387,6 +454,13 @@ class DistributedFrame:
         return self.flush()
 
     def timed_exchange(self):
+        """(see _timed_exchange); the renderer is back on the caller's stream after it."""
+        try:
+            return self._timed_exchange()
+        finally:
+            self.r.set_stream(self.caller)
+
+    def _timed_exchange(self):
         """One frame with its steps run one after another and each timed alone
         (nothing pipelined): this rank's render, the RGB8 pack, then -- once
         every rank has packed (barrier) -- the gather, and on rank 0 the
@@ -399,7 +473,7 @@ class DistributedFrame:
         import torch
         import torch.distributed as dist
 
-        p, st, slot = self.plan, self.streams[0], 0
+        st, slot = self.streams[0], 0
         dev = torch.device(f"cuda:{self.r.device}")
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         self.flush()

@@ -31,7 +31,25 @@ CONFIGS = {  # scene, W, H, max steps, pose
 }
 
 
-def per_frame_ms(r, torch, plan, rank, frames):
+def cumask_stream(torch):
+    """A HIP stream created with an all-CU mask: the runtime gives a CU-masked
+    stream a hardware queue of its own instead of sharing the least-used one."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask: {rc}")
+    return torch.cuda.ExternalStream(st.value)
+
+
+STREAM_KIND = "pool"
+
+
+def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
     """Rank's pipelined per-frame compute: render (RGBA8) + pack (RGB8) on two
     alternating streams, `frames` frames, wall time / frames."""
     p = plan
@@ -39,16 +57,23 @@ def per_frame_ms(r, torch, plan, rank, frames):
     if n == 0:
         return 0.0, 0.0
     W = p.W
-    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    if STREAM_KIND == "cumask":
+        streams = [cumask_stream(torch) for _ in range(nstreams)]
+    elif STREAM_KIND == "probed" and nstreams > 1:  # as DistributedFrame picks them
+        from raymarching_amd.frame import concurrent_streams
+        streams = concurrent_streams(torch.device("cuda:0"), nstreams)
+    else:
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     loc = [torch.empty((n, W), dtype=torch.int32, device="cuda") for _ in streams]
     wire = [torch.empty((n, 3 * W), dtype=torch.uint8, device="cuda") for _ in streams]
 
     def one(i):
-        st = streams[i % 2]
+        k = i % nstreams
+        st = streams[k]
         with torch.cuda.stream(st):
             r.set_stream(st)
-            r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[i % 2])
-            r.pack_rgb8(loc[i % 2], out=wire[i % 2])
+            r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[k])
+            r.pack_rgb8(loc[k], out=wire[k])
         r.set_stream(streams[0])
 
     t_end = time.time() + 0.3
@@ -92,10 +117,15 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--frames", type=int, default=24)
     ap.add_argument("--band", type=int, default=16)
+    ap.add_argument("--streams", type=int, default=2, help="frames in flight per rank (HIP streams)")
+    ap.add_argument("--even-only", action="store_true")
+    ap.add_argument("--stream-kind", default="probed", choices=["pool", "cumask", "probed"])
     ap.add_argument("--link-gbs", type=float, default=64.0,
                     help="assumed xGMI rate of one link, one direction, as RCCL point-to-point achieves it (GB/s)")
     args = ap.parse_args()
     import torch
+    global STREAM_KIND
+    STREAM_KIND = args.stream_kind
 
     import raymarching_amd as rm
     from bench import balanced_runs
@@ -111,15 +141,15 @@ def main():
     link_bpms = args.link_gbs * 1e6  # bytes per ms
     for N in [int(x) for x in args.ns.split(",")]:
         even = ShardPlan(W, H, args.band if N > 1 else H, N, None if N > 1 else (H,))
-        per = [per_frame_ms(r, torch, even, q, args.frames) for q in range(N)]
+        per = [per_frame_ms(r, torch, even, q, args.frames, args.streams) for q in range(N)]
         d = deinterleave_ms(r, torch, even) if N > 1 else 0.0
         rows = {"even": (even, per, d)}
-        if N > 1:
+        if N > 1 and not args.even_only:
             ex = {"render_ms": [x[0] for x in per], "gather_ms": max(even.count(q) for q in range(1, N)) * 3 * W
                   / link_bpms, "deinterleave_ms": d}
             runs, model = balanced_runs(N, args.band, H, ex)
             bal = ShardPlan(W, H, args.band, N, tuple(runs))
-            perb = [per_frame_ms(r, torch, bal, q, args.frames) for q in range(N)]
+            perb = [per_frame_ms(r, torch, bal, q, args.frames, args.streams) for q in range(N)]
             rows["balanced"] = (bal, perb, deinterleave_ms(r, torch, bal))
         for name, (plan, pr, dms) in rows.items():
             wire = [plan.count(q) * 3 * W for q in range(N)]
@@ -127,7 +157,7 @@ def main():
             compute = [pr[0][0] + dms] + [x[0] for x in pr[1:]]
             frame = max(max(compute), link)
             print(json.dumps({
-                "config": args.config, "N": N, "split": name, "runs": list(plan.part_runs),
+                "config": args.config, "N": N, "split": name, "streams": args.streams, "stream_kind": args.stream_kind, "runs": list(plan.part_runs),
                 "per_rank_frame_ms": [round(x[0], 4) for x in pr],
                 "per_rank_kernel_ms": [round(x[1], 4) for x in pr],
                 "deinterleave_ms": round(dms, 4), "wire_bytes": wire, "link_gbs_assumed": args.link_gbs,
