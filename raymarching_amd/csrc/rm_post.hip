@@ -135,6 +135,7 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #endif
 constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
 constexpr int FXL_MAX_DIM = 1 << 20;
+static_assert((FXL_TY & (FXL_TY - 1)) == 0 && FXL_TY <= 64, "fy_lane: one lane per tile row");
 __device__ __forceinline__ int clamp_to(int v, int hi) {  // v_med3_i32(v, 0, hi)
     int r;
     asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "v"(hi));
@@ -191,21 +192,25 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     const int x = x0 + lane;
     const float fx = ((float)x + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
     // a span tap: post.frag's float address (NEAREST), then the staged texel
+    // (block row * FXL_W as a 24-bit multiply: the row is clamped into the block)
     auto span_tap = [&](float u, float v) -> RGB {
         const int gx = clamp_to(floor_i32(u * (float)W) - tx0, FXL_W - 1);
         const int gy = clamp_to(floor_i32(v * (float)H) - ty0, FXL_H - 1);
-        return rgb(stex[gy * FXL_W + gx]);
+        return rgb(stex[__umul24(gy, FXL_W) + gx]);
     };
+    // fy of row y0 + l in lane l (rows past the frame: the clamped row), one
+    // correctly rounded division per tile instead of one per row; a row reads
+    // its lane's value as a wave-uniform scalar
+    const float fy_lane = 1.0f - ((float)min(y0 + (lane & (FXL_TY - 1)), H - 1) + 0.5f) / (float)H;
     // one pixel of row y0 + ly (its value; rows past the frame are computed on a
     // clamped row and not stored)
     auto pixel = [&](int ly) -> uint32_t {
         const int y = min(y0 + ly, H - 1);
-        // centre texel (x, H-1-y) in the block (rows H-1-y-ty0 = TY-1-(y-y0)+HALO)
         const int m = (FXL_TY - 1 - (y - y0) + FXL_HALO) * FXL_W + (lane + FXL_HALO);
         const float lNW = slum[m - FXL_W - 1], lNE = slum[m - FXL_W + 1], lSW = slum[m + FXL_W - 1];
         const float lSE = slum[m + FXL_W + 1], lM = slum[m];
         const uint32_t tM = stex[m];
-        const float fy = 1.0f - ((float)y + 0.5f) / (float)H;
+        const float fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_lane), ly));
         const float lMin = fminf(lM, fminf(fminf(lNW, lNE), fminf(lSW, lSE)));
         const float lMax = fmaxf(lM, fmaxf(fmaxf(lNW, lNE), fmaxf(lSW, lSE)));
         float dx = -((lNW + lNE) - (lSW + lSE));

@@ -1,0 +1,27 @@
+"""Post-pass driver for rocprofv3 runs: one 4096^2 scene-T RGBA8 frame, then
+`reps` passes of `fxaa` or `bloom` over it (tools/; not part of the product).
+Usage: post_probe.py fxaa|bloom [W] [H] [reps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch  # noqa: E402
+
+import raymarching_amd as rm  # noqa: E402
+
+which = sys.argv[1]
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+H = int(sys.argv[3]) if len(sys.argv) > 3 else W
+reps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+r = rm.Renderer(0)
+r.load_scene("template.frag")
+r.set_pose(*[rm.POSES["P0"][k] for k in ("pos", "mouse", "time")])
+r.set_params(max_steps=256, count_evals=0)
+frame = r.render_rgba8(W, H)
+out = torch.empty_like(frame)
+fn = getattr(r, which)
+for _ in range(reps):
+    fn(frame, out=out)
+torch.cuda.synchronize()
+print("post probe done", which, W, H, reps)
+r.close()
