@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Time the FXAA post pass of librm.so builds side by side (tools/build_variants.sh
-variants; one process per library, RM_LIB) over one 4096^2 scene-T RGBA8
-frame: median of 7 batches of 20 passes.  Usage: post_variant_ab.py lib.so ..."""
+"""Time a post pass (FXAA, or bloom with POST=bloom) of librm.so builds side by
+side (tools/build_variants.sh variants; one process per library, RM_LIB) over
+one 4096^2 scene-T RGBA8 frame: median of 7 batches of 20 passes.
+Usage: [POST=bloom] post_variant_ab.py lib.so ..."""
 import os
 import subprocess
 import sys
@@ -15,17 +16,18 @@ r.load_scene(rm.SCENE_FILES["T"])
 p = rm.POSES["P0"]; r.set_pose(p["pos"], p["mouse"], p["time"]); r.set_params(max_steps=256)
 f = r.render_rgba8(4096, 4096)
 out = torch.empty_like(f)
-ref = r.fxaa(f).clone()
+fn = getattr(r, sys.argv[2])
+ref = fn(f).clone()
 ms = []
 for _ in range(7):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(20):
-        r.fxaa(f, out=out)
+        fn(f, out=out)
     e1.record(); e1.synchronize()
     ms.append(e0.elapsed_time(e1) / 20)
-print(sys.argv[1], "fxaa_ms", sorted(ms)[3], "same_as_first", bool(torch.equal(out, ref)), flush=True)
+print(sys.argv[1], sys.argv[2] + "_ms", sorted(ms)[3], "same_as_first", bool(torch.equal(out, ref)), flush=True)
 '''
 for lib in sys.argv[1:]:
-    subprocess.run([sys.executable, "-c", CHILD, os.path.basename(lib)],
+    subprocess.run([sys.executable, "-c", CHILD, os.path.basename(lib), os.environ.get("POST", "fxaa")],
                    env=dict(os.environ, RM_LIB=os.path.abspath(lib)), timeout=120, check=True)
