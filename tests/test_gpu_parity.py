@@ -472,6 +472,26 @@ def test_c3_4096_properties(R, torch_cuda):
     assert torch.isfinite(img).all()
     assert torch.all(img[..., 3] == 1.0)
     assert torch.equal(R.render(4096, 4096), img)
+    # the balanced multi-GPU splits bench.py can choose: every
+    # part through the timed RGBA8 kernel in adaptive order (after repeated
+    # launches), the RGB8 wire back to back, rm_deinterleave_cycle_rgb8
+    ref8 = R.pack_rgba8(img)
+    R.set_params(schedule=1)
+    for runs in ((25, 16), (15,) + (16,) * 7):
+        wplan = ShardPlan(4096, 4096, 16, len(runs), runs)
+        wire = torch.empty((4096, 3 * 4096), dtype=torch.uint8, device="cuda")
+        base = wplan.part_bases()
+        for s in range(len(runs)):
+            n = wplan.count(s)
+            loc = torch.empty((n, 4096), dtype=torch.int32, device="cuda")
+            for _ in range(10):
+                R.render_cycle_rows(4096, 4096, wplan.cycle, wplan.offsets[s], runs[s], 0, n, loc)
+            _, st = R.render_cycle_rows(4096, 4096, wplan.cycle, wplan.offsets[s], runs[s], 0, n, loc, stats=True)
+            assert st["dispatch"] == "adaptive", st
+            R.pack_rgb8(loc, out=wire[base[s]: base[s] + n])
+        frame8 = R.deinterleave_cycle_rgb8(4096, 4096, wplan.cycle, list(wplan.offsets), list(runs),
+                                           [b * 3 * 4096 for b in base], wire)
+        assert torch.equal(frame8, ref8), runs
 
 
 def test_c5_8192_scene_O(R, torch_cuda):
