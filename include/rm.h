@@ -329,6 +329,14 @@ rm_status rm_comm_info(const rm_comm *comm, int *nranks, int *rank, int *uses_rc
 rm_status rm_render_sharded(rm_comm *comm, int W, int H, int band, uint32_t *frame, rm_stats *stats);
 rm_status rm_render_sharded_all(rm_comm *const *comms, int n, int W, int H, int band, uint32_t *frame,
                                 rm_stats *stats);
+/* The same with weighted parts instead of bands: runs[r] >= 1 rows of every
+ * cycle of sum(runs) rows go to rank r, in rank order (rm_cycle_rows); the
+ * parts cross the wire unpadded (grouped ncclSend/ncclRecv) and rank 0
+ * rebuilds the frame with rm_deinterleave_cycle_rgb8.  Every rank passes the
+ * same runs (nranks entries). */
+rm_status rm_render_sharded_runs(rm_comm *comm, int W, int H, const int *runs, uint32_t *frame, rm_stats *stats);
+rm_status rm_render_sharded_runs_all(rm_comm *const *comms, int n, int W, int H, const int *runs, uint32_t *frame,
+                                     rm_stats *stats);
 
 /* Message of the last failing call on ctx ("" if none). */
 const char *rm_last_error(rm_ctx *ctx);

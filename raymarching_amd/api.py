@@ -374,23 +374,31 @@ class Comm:
         check(lib().rm_comm_init_all(hs, ctxs, n), renderers[0]._ctx)
         return [Comm(r, n, i, _handle=ctypes.c_void_p(hs[i])) for i, r in enumerate(renderers)]
 
-    def render(self, W: int, H: int, band: int = 16, frame=None, stats: bool = False):
+    def render(self, W: int, H: int, band: int = 16, frame=None, stats: bool = False, runs=None):
         """One sharded frame (collective over the ranks).  Rank 0 gets the
-        [H, W] RGBA8 (int32 words) frame, the others None."""
+        [H, W] RGBA8 (int32 words) frame, the others None.  runs: weighted
+        parts (rm_render_sharded_runs, one run per rank) instead of bands."""
         torch = _torch()
         if self.rank == 0 and frame is None:
             frame = torch.empty((H, W), dtype=torch.int32, device=f"cuda:{self.r.device}")
         if frame is not None:
             _check_out(frame, H * W)
         s = RmStats()
-        check(lib().rm_render_sharded(self._h, int(W), int(H), int(band),
-                                      self.r._ptr(frame) if frame is not None else None,
-                                      ctypes.byref(s) if stats else None), self.r._ctx)
+        fp = self.r._ptr(frame) if frame is not None else None
+        sp = ctypes.byref(s) if stats else None
+        if runs is not None:
+            if len(runs) != self.nranks:
+                raise ValueError(f"runs needs {self.nranks} entries")
+            check(lib().rm_render_sharded_runs(self._h, int(W), int(H), (ctypes.c_int * len(runs))(*runs), fp, sp),
+                  self.r._ctx)
+        else:
+            check(lib().rm_render_sharded(self._h, int(W), int(H), int(band), fp, sp), self.r._ctx)
         return (frame, s.as_dict()) if stats else frame
 
     @staticmethod
-    def render_all(comms, W: int, H: int, band: int = 16, frame=None, stats: bool = False):
-        """rm_render_sharded_all over the communicators of init_all."""
+    def render_all(comms, W: int, H: int, band: int = 16, frame=None, stats: bool = False, runs=None):
+        """rm_render_sharded_all (or, with runs, rm_render_sharded_runs_all)
+        over the communicators of init_all."""
         torch = _torch()
         n = len(comms)
         if frame is None:
@@ -398,8 +406,14 @@ class Comm:
         _check_out(frame, H * W)
         hs = (ctypes.c_void_p * n)(*[c._h.value for c in comms])
         st = (RmStats * n)()
-        check(lib().rm_render_sharded_all(hs, n, int(W), int(H), int(band), comms[0].r._ptr(frame),
-                                          st if stats else None), comms[0].r._ctx)
+        if runs is not None:
+            if len(runs) != n:
+                raise ValueError(f"runs needs {n} entries")
+            check(lib().rm_render_sharded_runs_all(hs, n, int(W), int(H), (ctypes.c_int * n)(*runs),
+                                                   comms[0].r._ptr(frame), st if stats else None), comms[0].r._ctx)
+        else:
+            check(lib().rm_render_sharded_all(hs, n, int(W), int(H), int(band), comms[0].r._ptr(frame),
+                                              st if stats else None), comms[0].r._ctx)
         return (frame, [x.as_dict() for x in st]) if stats else frame
 
     @property

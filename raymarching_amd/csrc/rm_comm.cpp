@@ -92,6 +92,10 @@ struct rm_comm {
     // render start / render end / gather end / de-interleave end (rm_stats)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     int rows_mine = 0, rows_per_shard = 0;
+    // weighted parts (rm_render_sharded_runs): every rank's rows and the byte
+    // offset of its rows in the unpadded gathered buffer
+    bool weighted = false;
+    std::vector<int> rows_of, base_of;
 };
 
 namespace {
@@ -140,24 +144,72 @@ rm_status comm_new(rm_comm **out, rm_ctx *ctx, int nranks, int rank) {
     return RM_OK;
 }
 
+// How the frame's rows are dealt: round-robin bands of `band` rows, or (runs
+// non-null) weighted cyclic parts, rank r owning a run of runs[r] rows in every
+// cycle of sum(runs) rows, the runs in rank order.
+struct Split {
+    int band = 0;
+    const int *runs = nullptr;
+    int cycle = 0;
+    std::vector<int> off;
+};
+rm_status make_split(rm_comm *c, int band, const int *runs, Split &sp) {
+    sp.band = band;
+    sp.runs = runs;
+    if (!runs) return band > 0 ? RM_OK : RM_ERR_INVALID_ARGUMENT;
+    long long cyc = 0;
+    sp.off.assign(c->nranks, 0);
+    for (int r = 0; r < c->nranks; r++) {
+        if (runs[r] < 1) return RM_ERR_INVALID_ARGUMENT;
+        sp.off[r] = (int)cyc;
+        cyc += runs[r];
+        if (cyc > 0x7fffffffLL) return RM_ERR_INVALID_ARGUMENT;
+    }
+    sp.cycle = (int)cyc;
+    return RM_OK;
+}
+
 // render + pack this rank's rows (async on the ctx stream)
-rm_status enqueue_local(rm_comm *c, int W, int H, int band) {
+rm_status enqueue_local(rm_comm *c, int W, int H, const Split &sp) {
     rm_ctx *ctx = c->ctx;
-    rm_shard_layout L;
-    rm_status st = rm_sharded_layout(W, H, band, c->nranks, c->rank, &L);
-    if (st != RM_OK) return comm_fail(c, st, "rm_render_sharded: bad size/band");
-    const int n = L.rows_mine;
-    c->rows_mine = n;
-    c->rows_per_shard = L.rows_per_shard;
+    rm_status st = RM_OK;
+    size_t wire_bytes = 0, gathered_bytes = 0;
+    c->weighted = sp.runs != nullptr;
+    if (!c->weighted) {
+        rm_shard_layout L;
+        st = rm_sharded_layout(W, H, sp.band, c->nranks, c->rank, &L);
+        if (st != RM_OK) return comm_fail(c, st, "rm_render_sharded: bad size/band");
+        c->rows_mine = L.rows_mine;
+        c->rows_per_shard = L.rows_per_shard;
+        wire_bytes = (size_t)L.wire_bytes;
+        gathered_bytes = (size_t)L.gathered_bytes;
+    } else {
+        c->rows_of.assign(c->nranks, 0);
+        c->base_of.assign(c->nranks, 0);
+        int total = 0;
+        for (int r = 0; r < c->nranks; r++) {
+            st = rm_cycle_rows(H, sp.cycle, sp.off[r], sp.runs[r], &c->rows_of[r]);
+            if (st != RM_OK) return comm_fail(c, st, "rm_render_sharded_runs: bad size/runs");
+            c->base_of[r] = total;
+            total += c->rows_of[r];
+        }
+        c->rows_mine = c->rows_of[c->rank];
+        c->rows_per_shard = c->rows_mine;
+        wire_bytes = (size_t)c->rows_mine * 3 * W;
+        gathered_bytes = (size_t)H * 3 * W;  // every row once, rank by rank
+    }
+    const int n = c->rows_mine;
     if (hipSetDevice(rm_internal_device(ctx)) != hipSuccess) return comm_fail(c, RM_ERR_DEVICE, "hipSetDevice");
-    st = grow(c, c->band, c->band_bytes, (size_t)L.rows_per_shard * W * 4);
-    if (st == RM_OK) st = grow(c, c->wire, c->wire_bytes, (size_t)L.wire_bytes);
-    if (st == RM_OK && c->rank == 0 && c->nc) st = grow(c, c->gathered, c->gathered_bytes, (size_t)L.gathered_bytes);
+    st = grow(c, c->band, c->band_bytes, (size_t)c->rows_per_shard * W * 4);
+    if (st == RM_OK) st = grow(c, c->wire, c->wire_bytes, wire_bytes);
+    if (st == RM_OK && c->rank == 0 && c->nc) st = grow(c, c->gathered, c->gathered_bytes, gathered_bytes);
     if (st != RM_OK) return st;
     hipStream_t s = rm_internal_stream(ctx);
     if (hipEventRecord(c->ev0, s) != hipSuccess) return comm_fail(c, RM_ERR_DEVICE, "hipEventRecord");
     if (n > 0) {
-        st = rm_render_band_rgba8(ctx, W, H, band, c->nranks, c->rank, c->band, nullptr);
+        st = c->weighted ? rm_render_cycle_rows_rgba8(ctx, W, H, sp.cycle, sp.off[c->rank], sp.runs[c->rank], 0, n,
+                                                      c->band, nullptr)
+                         : rm_render_band_rgba8(ctx, W, H, sp.band, c->nranks, c->rank, c->band, nullptr);
         if (st != RM_OK) return st;
     }
     if (hipEventRecord(c->ev1, s) != hipSuccess) return comm_fail(c, RM_ERR_DEVICE, "hipEventRecord");
@@ -180,6 +232,26 @@ rm_status enqueue_gather_ops(rm_comm *c, int W) {
     rm::TraceRange range("rm_gather");
     Rccl *R = rccl();
     hipStream_t s = rm_internal_stream(c->ctx);
+    if (c->weighted) {  // unequal parts: grouped point-to-point, unpadded
+        const size_t row = (size_t)3 * W;
+        rm_status st = nccl_check(c, R->GroupStart(), "ncclGroupStart");
+        if (st != RM_OK) return st;
+        if (c->rank == 0) {
+            for (int r = 1; r < c->nranks && st == RM_OK; r++)
+                if (c->rows_of[r] > 0)
+                    st = nccl_check(c, R->Recv(c->gathered + (size_t)c->base_of[r] * row, (size_t)c->rows_of[r] * row,
+                                               kNcclUint8, r, c->nc, s), "ncclRecv");
+        } else if (c->rows_mine > 0) {
+            st = nccl_check(c, R->Send(c->wire, (size_t)c->rows_mine * row, kNcclUint8, 0, c->nc, s), "ncclSend");
+        }
+        rm_status st2 = nccl_check(c, R->GroupEnd(), "ncclGroupEnd");
+        if (st != RM_OK) return st;
+        if (st2 != RM_OK) return st2;
+        if (c->rank == 0 && c->rows_mine > 0 &&
+            hipMemcpyAsync(c->gathered, c->wire, (size_t)c->rows_mine * row, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return comm_fail(c, RM_ERR_DEVICE, "gather copy");
+        return RM_OK;
+    }
     const size_t bytes = (size_t)c->rows_per_shard * 3 * W;
     if (R->Gather)
         return nccl_check(c, R->Gather(c->wire, c->rank == 0 ? c->gathered : nullptr, bytes, kNcclUint8, 0, c->nc, s),
@@ -201,12 +273,18 @@ rm_status enqueue_gather_ops(rm_comm *c, int W) {
     return RM_OK;
 }
 
-rm_status finish(rm_comm *c, int W, int H, int band, uint32_t *frame, rm_stats *stats) {
+rm_status finish(rm_comm *c, int W, int H, const Split &sp, uint32_t *frame, rm_stats *stats) {
     rm_status st = RM_OK;
     rm::TraceRange range("rm_deinterleave");
-    if (c->rank == 0)
-        st = rm_deinterleave_rgb8(c->ctx, W, H, band, c->nranks, c->rows_per_shard,
+    if (c->rank == 0 && c->weighted) {
+        std::vector<int64_t> bytes(c->nranks);
+        for (int r = 0; r < c->nranks; r++) bytes[r] = (int64_t)c->base_of[r] * 3 * W;
+        st = rm_deinterleave_cycle_rgb8(c->ctx, W, H, sp.cycle, c->nranks, sp.off.data(), sp.runs, bytes.data(),
+                                        c->nc ? c->gathered : c->wire, frame);
+    } else if (c->rank == 0) {
+        st = rm_deinterleave_rgb8(c->ctx, W, H, sp.band, c->nranks, c->rows_per_shard,
                                   c->nc ? c->gathered : c->wire, frame);
+    }
     if (st != RM_OK) return st;
     if (c->rank == 0 && hipEventRecord(c->ev3, rm_internal_stream(c->ctx)) != hipSuccess)
         return comm_fail(c, RM_ERR_DEVICE, "hipEventRecord");
@@ -349,24 +427,32 @@ rm_status rm_comm_info(const rm_comm *comm, int *nranks, int *rank, int *uses_rc
     return RM_OK;
 }
 
-rm_status rm_render_sharded(rm_comm *comm, int W, int H, int band, uint32_t *frame, rm_stats *stats) {
+}  // extern "C"
+
+namespace {
+
+rm_status render_sharded(rm_comm *comm, int W, int H, int band, const int *runs, uint32_t *frame, rm_stats *stats) {
     if (!comm) return RM_ERR_INVALID_ARGUMENT;
-    if (W <= 0 || H <= 0 || band <= 0) return comm_fail(comm, RM_ERR_INVALID_ARGUMENT, "rm_render_sharded: bad size");
+    Split sp;
+    if (W <= 0 || H <= 0 || make_split(comm, band, runs, sp) != RM_OK)
+        return comm_fail(comm, RM_ERR_INVALID_ARGUMENT, "rm_render_sharded: bad size/band/runs");
     if (comm->rank == 0 && !frame) return comm_fail(comm, RM_ERR_INVALID_ARGUMENT, "rm_render_sharded: null frame on rank 0");
-    rm_status st = enqueue_local(comm, W, H, band);
+    rm_status st = enqueue_local(comm, W, H, sp);
     if (st == RM_OK) st = enqueue_gather(comm, W);
-    if (st == RM_OK) st = finish(comm, W, H, band, frame, stats);
+    if (st == RM_OK) st = finish(comm, W, H, sp, frame, stats);
     return st;
 }
 
-rm_status rm_render_sharded_all(rm_comm *const *comms, int n, int W, int H, int band, uint32_t *frame,
-                                rm_stats *stats) {
+rm_status render_sharded_all(rm_comm *const *comms, int n, int W, int H, int band, const int *runs, uint32_t *frame,
+                             rm_stats *stats) {
     if (!comms || n < 1 || !frame) return RM_ERR_INVALID_ARGUMENT;
     for (int i = 0; i < n; i++)
         if (!comms[i] || comms[i]->nranks != n || comms[i]->rank != i) return RM_ERR_INVALID_ARGUMENT;
-    if (W <= 0 || H <= 0 || band <= 0) return comm_fail(comms[0], RM_ERR_INVALID_ARGUMENT, "rm_render_sharded_all: bad size");
+    Split sp;
+    if (W <= 0 || H <= 0 || make_split(comms[0], band, runs, sp) != RM_OK)
+        return comm_fail(comms[0], RM_ERR_INVALID_ARGUMENT, "rm_render_sharded_all: bad size/band/runs");
     for (int i = 0; i < n; i++) {  // every device renders its rows concurrently
-        rm_status st = enqueue_local(comms[i], W, H, band);
+        rm_status st = enqueue_local(comms[i], W, H, sp);
         if (st != RM_OK) return st;
     }
     if (n == 1) {
@@ -394,10 +480,35 @@ rm_status rm_render_sharded_all(rm_comm *const *comms, int n, int W, int H, int 
     }
     (void)hipSetDevice(rm_internal_device(comms[0]->ctx));
     for (int i = 0; i < n; i++) {
-        rm_status st = finish(comms[i], W, H, band, i == 0 ? frame : nullptr, stats ? stats + i : nullptr);
+        rm_status st = finish(comms[i], W, H, sp, i == 0 ? frame : nullptr, stats ? stats + i : nullptr);
         if (st != RM_OK) return st;
     }
     return RM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rm_status rm_render_sharded(rm_comm *comm, int W, int H, int band, uint32_t *frame, rm_stats *stats) {
+    return render_sharded(comm, W, H, band, nullptr, frame, stats);
+}
+
+rm_status rm_render_sharded_all(rm_comm *const *comms, int n, int W, int H, int band, uint32_t *frame,
+                                rm_stats *stats) {
+    return render_sharded_all(comms, n, W, H, band, nullptr, frame, stats);
+}
+
+rm_status rm_render_sharded_runs(rm_comm *comm, int W, int H, const int *runs, uint32_t *frame, rm_stats *stats) {
+    if (!comm) return RM_ERR_INVALID_ARGUMENT;
+    if (!runs) return comm_fail(comm, RM_ERR_INVALID_ARGUMENT, "rm_render_sharded_runs: null runs");
+    return render_sharded(comm, W, H, 0, runs, frame, stats);
+}
+
+rm_status rm_render_sharded_runs_all(rm_comm *const *comms, int n, int W, int H, const int *runs, uint32_t *frame,
+                                     rm_stats *stats) {
+    if (!runs) return RM_ERR_INVALID_ARGUMENT;
+    return render_sharded_all(comms, n, W, H, 0, runs, frame, stats);
 }
 
 }  // extern "C"

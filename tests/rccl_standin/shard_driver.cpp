@@ -46,6 +46,7 @@ const Pose kPoses[2] = {
      57.79888153076172f}};
 
 int g_W, g_H, g_band;
+std::vector<int> g_runs;  // BAND given as "r0,r1,...": weighted parts (rm_render_sharded_runs*)
 std::string g_scene;
 
 bool setup(rm_ctx *c, const Pose &p) {
@@ -109,7 +110,10 @@ int run_all(int n) {
     for (int f = 0; f < 2; f++) {
         for (int i = 0; i < n; i++)
             if (!setup(ctx[i], kPoses[f])) return 1;
-        if (rm_render_sharded_all(comm.data(), n, g_W, g_H, g_band, frame, st.data()) != RM_OK) {
+        const rm_status rs = g_runs.empty() ? rm_render_sharded_all(comm.data(), n, g_W, g_H, g_band, frame, st.data())
+                                            : rm_render_sharded_runs_all(comm.data(), n, g_W, g_H, g_runs.data(), frame,
+                                                                         st.data());
+        if (rs != RM_OK) {
             std::fprintf(stderr, "rm_render_sharded_all: %s\n", rm_last_error(ctx[0]));
             return 1;
         }
@@ -172,7 +176,10 @@ int rank_worker(Shared *sh, int n, int rank) {
     rm_stats st{};
     for (int f = 0; f < 2; f++) {
         if (!setup(ctx, kPoses[f])) return 1;
-        if (rm_render_sharded(comm, g_W, g_H, g_band, frame, rank == 0 ? &st : nullptr) != RM_OK) {
+        const rm_status rs = g_runs.empty()
+                                 ? rm_render_sharded(comm, g_W, g_H, g_band, frame, rank == 0 ? &st : nullptr)
+                                 : rm_render_sharded_runs(comm, g_W, g_H, g_runs.data(), frame, rank == 0 ? &st : nullptr);
+        if (rs != RM_OK) {
             std::fprintf(stderr, "rank %d rm_render_sharded: %s\n", rank, rm_last_error(ctx));
             return 1;
         }
@@ -242,6 +249,15 @@ int main(int argc, char **argv) {
     g_W = std::atoi(argv[3]);
     g_H = std::atoi(argv[4]);
     g_band = std::atoi(argv[5]);
+    if (std::strchr(argv[5], ',')) {
+        for (const char *q = argv[5]; *q;) {
+            g_runs.push_back(std::atoi(q));
+            q = std::strchr(q, ',');
+            q = q ? q + 1 : "";
+        }
+        if ((int)g_runs.size() != n) return 2;
+        g_band = g_runs[0];
+    }
     g_scene = argv[6];
     if (n < 1 || n > 16 || g_W < 1 || g_H < 1 || g_band < 1) return 2;
     if (mode == "all") return run_all(n);

@@ -102,6 +102,24 @@ def test_render_sharded_n_processes(torch_cuda, variant, n, W, H, band, scene):
     assert (g, r) == ((2, 0) if variant == "gather" else (0, 2 * (n - 1))), res
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["all", "ranks"])
+@pytest.mark.parametrize("n,W,H,runs,scene", [(2, 200, 120, "25,16", "template.frag"),
+                                              (3, 131, 77, "2,9,4", "output_shader.frag"),
+                                              (8, 160, 120, "15,8,8,8,8,8,8,8", "template.frag")])
+def test_render_sharded_runs(torch_cuda, mode, n, W, H, runs, scene):
+    """rm_render_sharded_runs[_all]: weighted parts (rank r owns a run of
+    runs[r] rows per cycle) gathered unpadded with grouped send/recv, the
+    frame rebuilt by rm_deinterleave_cycle_rgb8, equal to rm_render_rgba8."""
+    res = run_driver(mode, n, W, H, runs, scene, standin="gather")
+    assert res["equal"] and res["frames"] == 2 and res["uses_rccl"] == 1, res
+    k, g, d = res["root_ms"]
+    assert k > 0 and g > 0 and d > 0, res
+    g, s, r, _ = res["standin_stats"]
+    # no ncclGather for unequal parts: every non-root part is one send/recv pair
+    assert g == 0 and r == 2 * (n - 1), res
+
+
 def _ngpus():
     import torch
     return torch.cuda.device_count()
