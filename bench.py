@@ -67,6 +67,9 @@ def parse():
                          "split that gives rank 0 (which receives every other rank's rows and de-interleaves) "
                          "a longer run per cycle, sized from the timed exchange, and keeps whichever plan ran "
                          "the untimed trial frames faster")
+    ap.add_argument("--wire", default="auto", choices=["auto", "rgb8", "delta"],
+                    help="N > 1: the RGB8 wire (3 B/px), the compressed wire (DeltaFrame: a lossless delta "
+                         "code per 64-pixel row segment), or 'auto': both in the untimed trial, the faster timed")
     ap.add_argument("--chunks", type=int, default=None,
                     help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
@@ -335,7 +338,7 @@ def main():
     import torch.distributed as dist
 
     import raymarching_amd as rm
-    from raymarching_amd.frame import DistributedFrame
+    from raymarching_amd.frame import DeltaFrame, DistributedFrame
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -400,42 +403,51 @@ def main():
         return float(tt.item())
 
     balance = None
-    if world > 1 and args.balance == "auto" and args.fmt == "rgba8":
-        # split calibration (untimed): one timed exchange of the even split,
-        # the balanced runs it implies, then trial frames of both plans
+    if world > 1 and args.fmt == "rgba8" and (args.balance == "auto" or args.wire != "rgb8"):
+        # plan calibration (untimed): candidate frames -- the even split over
+        # the RGB8 wire, the balanced split its timed exchange implies, the even
+        # split over the compressed wire -- each run for trial frames; the
+        # fastest is timed
         spin_up()
-        xs = [fr.timed_exchange() for _ in range(3)]
-        mine = torch.tensor([_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
-                                                                    "deinterleave_ms")],
-                            dtype=torch.float64, device=red_dev)
-        per = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(per, mine)
-        per = [[float(v) for v in x.cpu()] for x in per]
-        ex = {"render_ms": [x[0] for x in per], "pack_ms": [x[1] for x in per], "gather_ms": per[0][2],
-              "deinterleave_ms": per[0][3]}
-        runs, model = balanced_runs(world, args.band, H, ex)
-        even_ms = trial_ms(fr)
-        bal, bal_ms, err = None, float("inf"), None
-        try:
-            bal = DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt, chunks=chunks,
-                                   streams=args.streams, runs=runs)
-            bal_ms = trial_ms(bal)
-        except (RuntimeError, ValueError) as e:  # keep the even split; say why in the line
-            err = f"{type(e).__name__}: {e}"
-            torch.cuda.synchronize(dev)
-        chosen = "balanced" if bal_ms < even_ms else "even"
-        balance = {"mode": "auto", "chosen": chosen, "runs": runs if chosen == "balanced" else [args.band] * world,
-                   "trial_ms": {"even": even_ms, "balanced": bal_ms}, "balanced_runs": runs, "model": model,
-                   "note": "untimed trial frames (16 pipelined frames per plan, max over ranks) before the "
-                           "instrumented run and the warm-up; the timed frames use the chosen plan"}
-        if err is not None:
-            balance["error"] = err
-        if chosen == "balanced":
-            fr = bal
-        else:
-            del bal
+        cands, errors, runs, model = {}, {}, None, None
+
+        def build(name, make):
+            try:
+                f = make()
+                cands[name] = (f, trial_ms(f))
+            except (RuntimeError, ValueError) as e:  # keep the others; say why in the line
+                errors[name] = f"{type(e).__name__}: {e}"
+                torch.cuda.synchronize(dev)
+
+        if args.wire in ("auto", "rgb8"):
+            cands["even/rgb8"] = (fr, trial_ms(fr))
+            if args.balance == "auto":
+                xs = [fr.timed_exchange() for _ in range(3)]
+                mine = torch.tensor([_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
+                                                                            "deinterleave_ms")],
+                                    dtype=torch.float64, device=red_dev)
+                per = [torch.empty_like(mine) for _ in range(world)]
+                dist.all_gather(per, mine)
+                per = [[float(v) for v in x.cpu()] for x in per]
+                ex = {"render_ms": [x[0] for x in per], "pack_ms": [x[1] for x in per], "gather_ms": per[0][2],
+                      "deinterleave_ms": per[0][3]}
+                runs, model = balanced_runs(world, args.band, H, ex)
+                build("balanced/rgb8", lambda: DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt,
+                                                                chunks=chunks, streams=args.streams, runs=runs))
+        if args.wire in ("auto", "delta"):
+            build("even/delta", lambda: DeltaFrame(r, W, H, args.band, rank, world, streams=args.streams))
+        chosen = min(cands, key=lambda k: cands[k][1])
+        fr = cands[chosen][0]
+        balance = {"mode": f"balance {args.balance}, wire {args.wire}", "chosen": chosen,
+                   "runs": list(fr.plan.part_runs), "wire": fr.wire,
+                   "trial_ms": {k: v[1] for k, v in cands.items()}, "balanced_runs": runs, "model": model,
+                   "note": "untimed trial frames (16 pipelined frames per candidate, max over ranks) before the "
+                           "instrumented run and the warm-up; the timed frames use the chosen candidate"}
+        if errors:
+            balance["errors"] = errors
+        cands.clear()
     elif world > 1:
-        balance = {"mode": "even", "chosen": "even", "runs": [args.band] * world}
+        balance = {"mode": "even", "chosen": "even/" + fr.wire, "runs": [args.band] * world, "wire": fr.wire}
 
     def set_frame(i):  # walk: the pose of frame i (timed frames 0..K-1)
         if args.walk:
@@ -522,6 +534,10 @@ def main():
         # the pipelined frames overlap with the next frame's render
         xs = [fr.timed_exchange() for _ in range(5)]
         wire_row = fr.wires[0].stride(0) * fr.wires[0].element_size()  # bytes of one row on the wire
+        if fr.wire == "delta":  # the messages' measured sizes (the last timed exchange)
+            wire_sizes = [int(v) for v in xs[-1]["wire_bytes"]]
+        else:
+            wire_sizes = [fr.plan.count(q) * wire_row for q in range(world)]
         mine = torch.tensor([kern] + [_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
                                                                                 "deinterleave_ms")],
                             dtype=torch.float64, device=red_dev)
@@ -532,8 +548,9 @@ def main():
             "gather_ms": pr[0][3], "deinterleave_ms": pr[0][4], "pack_ms": pr[0][2],
             "kernel_ms_per_rank": [x[0] for x in pr], "gather_ms_per_rank": [x[3] for x in pr],
             "pack_ms_per_rank": [x[2] for x in pr],
-            "wire_bytes_per_rank": [fr.plan.count(q) * wire_row for q in range(world)],
-            "root_ingress_bytes": sum(fr.plan.count(q) for q in range(1, world)) * wire_row,
+            "wire_bytes_per_rank": wire_sizes,
+            "root_ingress_bytes": sum(wire_sizes[1:]),
+            "wire": fr.wire,
             "backend": args.backend,
             "note": "median of 5 frames whose steps run one after another, each timed alone after the timed "
                     "region: kernel_ms_per_rank = each rank's render kernel (11 synchronous launches), "
@@ -580,6 +597,7 @@ def main():
                             + (f"row bands of {args.band} over {world} GPU(s)" if fr.plan.runs is None else
                                f"weighted row runs {list(fr.plan.runs)} per cycle of {fr.plan.cycle} over "
                                f"{world} GPUs")
+                            + (f", {fr.wire} wire" if world > 1 else "")
                             + f", {args.fmt} frame on rank 0"
                             + (f", walking (camera +{args.walk_speed}/frame forward, u_time +{args.walk_dt:.4f} s/frame)"
                                if args.walk else ""),

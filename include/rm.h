@@ -287,6 +287,27 @@ rm_status rm_deinterleave_cycle_rgb8(rm_ctx *ctx, int W, int H, int cycle, int n
                                      const int *runs, const int64_t *part_bytes, const uint8_t *gathered,
                                      uint32_t *out);
 
+/* ---- Compressed wire of RGBA8 row parts ----
+ * A lossless delta code per 64-pixel row segment (first pixel, left
+ * differences as per-channel bit planes); alpha is not sent (the root stores
+ * 255).  rm_wire_encode: nrows packed RGBA8 rows -> msg (at most
+ * rm_wire_capacity bytes), using a caller-owned device workspace of
+ * rm_wire_workspace_bytes; the message size (also its first 8 bytes) is
+ * written to the device int64 *size_out when non-null (asynchronous, ctx
+ * stream).  rm_wire_decode: a message of nrows rows of the cyclic part
+ * (cycle, offset, run) into those rows of the W x H RGBA8 frame.
+ * rm_scatter_part_rgba8: a part's packed RGBA8 rows into their frame rows
+ * (the root's own part).  Capacity/workspace return -1 for bad sizes
+ * (W <= 2^18). */
+int64_t rm_wire_capacity(int W, int nrows);
+int64_t rm_wire_workspace_bytes(int W, int nrows);
+rm_status rm_wire_encode(rm_ctx *ctx, int W, int nrows, const uint32_t *rows, uint8_t *msg, void *workspace,
+                         int64_t *size_out);
+rm_status rm_wire_decode(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int nrows, const uint8_t *msg,
+                         uint32_t *frame);
+rm_status rm_scatter_part_rgba8(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int nrows,
+                                const uint32_t *rows, uint32_t *frame);
+
 /* ---- Multi-GPU: row-sharded frames over RCCL ----
  * The reference renders one frame on one GPU (main.cpp:196-207); here a frame's
  * rows are dealt to nranks GPUs in bands of `band` rows, round robin (rank r

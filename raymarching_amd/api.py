@@ -224,6 +224,41 @@ class Renderer:
                                                self._ptr(out)), self._ctx)
         return out
 
+    def wire_encode(self, rows, msg, workspace, size_out=None):
+        """Compressed wire of packed RGBA8 rows (int32 [n, W]) into the uint8
+        `msg` (>= wire_capacity bytes), with a uint8 `workspace` of
+        wire_workspace_bytes; size_out: optional int64 device tensor [1] that
+        receives the message size (asynchronously)."""
+        torch = _torch()
+        n, W = (int(rows.shape[0]), int(rows.shape[1])) if rows.dim() == 2 else (0, 0)
+        if rows.dtype != torch.int32 or not rows.is_contiguous() or rows.dim() != 2:
+            raise ValueError("wire_encode: rows must be contiguous int32 [n, W] RGBA8 words")
+        if msg.dtype != torch.uint8 or msg.numel() < wire_capacity(W, n) or not msg.is_contiguous():
+            raise ValueError("wire_encode: msg must be a contiguous uint8 tensor of wire_capacity bytes")
+        if workspace.numel() * workspace.element_size() < wire_workspace_bytes(W, n):
+            raise ValueError("wire_encode: workspace too small")
+        if size_out is not None and (size_out.dtype != torch.int64 or size_out.numel() < 1):
+            raise ValueError("wire_encode: size_out must be an int64 tensor")
+        check(lib().rm_wire_encode(self._ctx, W, n, self._ptr(rows), self._ptr(msg), self._ptr(workspace),
+                                   self._ptr(size_out) if size_out is not None else None), self._ctx)
+        return msg
+
+    def wire_decode(self, W, H, cycle, offset, run, nrows, msg, frame):
+        """A wire message of `nrows` rows of the cyclic part into the int32
+        [H, W] RGBA8 frame (alpha 255)."""
+        _check_out(frame, H * W)
+        check(lib().rm_wire_decode(self._ctx, int(W), int(H), int(cycle), int(offset), int(run), int(nrows),
+                                   self._ptr(msg), self._ptr(frame)), self._ctx)
+        return frame
+
+    def scatter_part_rgba8(self, W, H, cycle, offset, run, nrows, rows, frame):
+        """A part's packed RGBA8 rows (int32 [nrows, W]) into their frame rows."""
+        _check_out(frame, H * W)
+        _check_out(rows, nrows * W)
+        check(lib().rm_scatter_part_rgba8(self._ctx, int(W), int(H), int(cycle), int(offset), int(run), int(nrows),
+                                          self._ptr(rows), self._ptr(frame)), self._ctx)
+        return frame
+
     def render_band_rgba8(self, W, H, band, nshards, shard, out=None, stats=False):
         """render_band into RGBA8 words ([rows, W] int32)."""
         torch = _torch()
@@ -454,6 +489,21 @@ def _check_out(t, nfloats):
         ok, n, es = bool(t.flags["C_CONTIGUOUS"]), t.size, t.itemsize
     if not ok or n < nfloats or es != 4:
         raise ValueError(f"buffer must be contiguous 32-bit with >= {nfloats} elements")
+
+
+def wire_capacity(W: int, nrows: int) -> int:
+    """Largest wire message of nrows rows of W pixels (rm_wire_capacity)."""
+    v = int(lib().rm_wire_capacity(int(W), int(nrows)))
+    if v < 0:
+        raise ValueError("wire_capacity: bad size")
+    return v
+
+
+def wire_workspace_bytes(W: int, nrows: int) -> int:
+    v = int(lib().rm_wire_workspace_bytes(int(W), int(nrows)))
+    if v < 0:
+        raise ValueError("wire_workspace_bytes: bad size")
+    return v
 
 
 def cycle_rows(H: int, cycle: int, offset: int, run: int) -> int:

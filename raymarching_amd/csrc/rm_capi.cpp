@@ -958,6 +958,59 @@ rm_status rm_deinterleave_cycle_rgb8(rm_ctx *ctx, int W, int H, int cycle, int n
     return mark_done(ctx);
 }
 
+int64_t rm_wire_capacity(int W, int nrows) {
+    return (W <= 0 || W > (1 << 18) || nrows < 0) ? -1 : (int64_t)rm::wire_capacity(W, nrows);
+}
+
+int64_t rm_wire_workspace_bytes(int W, int nrows) {
+    return (W <= 0 || W > (1 << 18) || nrows < 0) ? -1 : (int64_t)rm::wire_workspace(W, nrows);
+}
+
+rm_status rm_wire_encode(rm_ctx *ctx, int W, int nrows, const uint32_t *rows, uint8_t *msg, void *workspace,
+                         int64_t *size_out) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (W <= 0 || W > (1 << 18) || nrows < 0 || !msg || !workspace || (nrows > 0 && !rows))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_encode: bad arguments");
+    if (!is_device_ptr(msg) || !is_device_ptr(workspace) || (nrows > 0 && !is_device_ptr(rows)) ||
+        (size_out && !is_device_ptr(size_out)))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_encode: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_wire_encode(rows, W, nrows, msg, workspace, reinterpret_cast<long long *>(size_out),
+                                          ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "wire encode launch");
+    return mark_done(ctx);
+}
+
+rm_status rm_wire_decode(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int nrows, const uint8_t *msg,
+                         uint32_t *frame) {
+    RowPart p;
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (W <= 0 || W > (1 << 18) || H <= 0 || !cycle_part(cycle, offset, run, p) || nrows < 0 ||
+        nrows > rows_of_part(H, p) || !msg || !frame)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_decode: bad arguments");
+    if (!is_device_ptr(msg) || !is_device_ptr(frame))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_decode: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_wire_decode(msg, nrows, W, cycle, offset, run, frame, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "wire decode launch");
+    return mark_done(ctx);
+}
+
+rm_status rm_scatter_part_rgba8(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int nrows,
+                                const uint32_t *rows, uint32_t *frame) {
+    RowPart p;
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (W <= 0 || H <= 0 || !cycle_part(cycle, offset, run, p) || nrows < 0 || nrows > rows_of_part(H, p) ||
+        !frame || (nrows > 0 && !rows))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_scatter_part_rgba8: bad arguments");
+    if (!is_device_ptr(frame) || (nrows > 0 && !is_device_ptr(rows)))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_scatter_part_rgba8: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_scatter_part(rows, nrows, W, cycle, offset, run, frame, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "scatter launch");
+    return mark_done(ctx);
+}
+
 rm_status rm_set_tile_order(rm_ctx *ctx, const uint32_t *order, int64_t n) {
     if (!ctx || n < 0 || (n > 0 && !order)) return RM_ERR_INVALID_ARGUMENT;
     RM_HIP(hipSetDevice(ctx->device));

@@ -49,6 +49,15 @@ hipError_t launch_deinterleave_cycle_rgb8(const uint8_t* gathered, uint32_t* out
 hipError_t launch_tile_order(const uint32_t* cost, int n, int gx, int radius, uint32_t* order, uint32_t* hist,
                              uint32_t* next, hipStream_t s);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
+// rm_wire.hip: the compressed RGB wire of RGBA8 row parts
+long long wire_capacity(int W, int n);
+long long wire_workspace(int W, int n);
+hipError_t launch_wire_encode(const uint32_t* rows, int W, int n, uint8_t* msg, void* workspace,
+                              long long* size_out, hipStream_t s);
+hipError_t launch_wire_decode(const uint8_t* msg, int n, int W, int cycle, int offset, int run, uint32_t* frame,
+                              hipStream_t s);
+hipError_t launch_scatter_part(const uint32_t* rows, int n, int W, int cycle, int offset, int run, uint32_t* frame,
+                               hipStream_t s);
 
 // bloom.frag's textureLod level pair and the mip levels 1..d2 it needs,
 // packed one after the other in a scratch buffer of `texels` 32-bit words

@@ -47,12 +47,12 @@ def test_bench_one_gpu_frame_check(torch_cuda, scene):
 def test_bench_two_ranks_gloo_rehearsal(torch_cuda):
     """Two ranks on one GPU over gloo: the whole multi-rank path of bench.py
     (row bands, RGB8 wire, gather, de-interleave) and its exchange figures."""
-    res = _run(_torchrun(2, SMALL + ["--backend", "gloo", "--balance", "even"]))
+    res = _run(_torchrun(2, SMALL + ["--backend", "gloo", "--balance", "even", "--wire", "rgb8"]))
     assert res["n_gpus"] == 2 and res["frame_check"]["result"] == "bit-exact", res
     assert len(res["kernel_ms_per_rank"]) == 2 and all(k > 0 for k in res["kernel_ms_per_rank"]), res
     assert res["gather_ms"] > 0 and res["deinterleave_ms"] > 0 and res["backend"] == "gloo", res
     assert res["root_ingress_bytes"] == 256 * 3 * 512 and res["wire_bytes_per_rank"] == [256 * 3 * 512] * 2, res
-    assert res["balance"] == {"mode": "even", "chosen": "even", "runs": [16, 16]}, res
+    assert res["balance"] == {"mode": "even", "chosen": "even/rgb8", "runs": [16, 16], "wire": "rgb8"}, res
 
 
 @pytest.mark.gpu
@@ -60,14 +60,24 @@ def test_bench_two_ranks_gloo_balanced(torch_cuda):
     """--balance auto: the host-staged gloo gather is slow, so the balanced
     split (rank 0 renders a longer run of every cycle) is sized from the timed
     exchange, wins the trial, and its frame is still bit-exact."""
-    res = _run(_torchrun(2, SMALL + ["--backend", "gloo", "--balance", "auto"]))
+    res = _run(_torchrun(2, SMALL + ["--backend", "gloo", "--balance", "auto", "--wire", "rgb8"]))
     b = res["balance"]
-    assert b["mode"] == "auto" and b["balanced_runs"][0] > 16 and b["balanced_runs"][1] == 16, res
+    assert b["chosen"] == "balanced/rgb8" and b["balanced_runs"][0] > 16 and b["balanced_runs"][1] == 16, res
     assert res["frame_check"]["result"] == "bit-exact", res
     runs = b["runs"]
     cyc = sum(runs)
     n1 = (512 // cyc) * runs[1] + min(max(512 % cyc - runs[0], 0), runs[1])
     assert res["root_ingress_bytes"] == n1 * 3 * 512 and sum(res["wire_bytes_per_rank"]) == 512 * 3 * 512, res
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_compressed_wire(torch_cuda):
+    """--wire delta: the compressed wire (DeltaFrame) end to end, bit-exact,
+    with fewer bytes into the root than the RGB8 wire's."""
+    res = _run(_torchrun(2, SMALL + ["--backend", "gloo", "--balance", "even", "--wire", "delta"]))
+    assert res["balance"]["chosen"] == "even/delta" and res["wire"] == "delta", res
+    assert res["frame_check"]["result"] == "bit-exact", res
+    assert 0 < res["root_ingress_bytes"] < 256 * 3 * 512, res
 
 
 @pytest.mark.gpu

@@ -920,3 +920,127 @@ def test_weighted_cycle_parts_rebuild_frame(R, torch_cuda, W, H, runs):
         R.deinterleave_cycle_rgb8(W, H, plan.cycle + 1, list(plan.offsets), list(runs), [0] * len(runs), gathered)
     with pytest.raises(rm.RmError):
         R.render_cycle_rows(W, H, 4, 3, 2, 0, 1, frame[:1])
+
+
+def _delta_worker(rank, world, port, runs, q):
+    import os as _os
+
+    import torch
+    import torch.distributed as dist
+
+    from raymarching_amd.frame import DeltaFrame
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = rm.Renderer(0)
+    setup(r, "T", POSES["P0"], 128)
+    r.set_params(count_evals=0)
+    fr = DeltaFrame(r, 96, 70, 8, rank, world, runs=runs)
+    for _ in range(3):
+        fr.submit()
+    frame = fr.flush()
+    x = fr.timed_exchange()
+    if rank == 0:
+        torch.cuda.synchronize()
+        q.put((frame.cpu().numpy(), fr.frame.cpu().numpy(), x["wire_bytes"]))
+    dist.barrier()
+    r.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("runs", [None, (13, 8)])
+def test_compressed_wire_frame_two_ranks_on_one_gpu(R, torch_cuda, runs):
+    """DeltaFrame over gloo (two ranks on cuda:0): the compressed wire's frame
+    equals a one-rank rm_render_rgba8 frame, after pipelined submits and after
+    the timed exchange."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_delta_worker, args=(r, 2, port, runs, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    frame, frame2, sizes = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    setup(R, "T", POSES["P0"], 128)
+    R.set_params(count_evals=0)
+    ref = R.render_rgba8(96, 70).cpu().numpy()
+    assert np.array_equal(frame, ref) and np.array_equal(frame2, ref)
+    assert sizes[0] == 0 and sizes[1] > 0
+
+
+@pytest.mark.parametrize("runs", [None, (13, 8)])
+def test_compressed_wire_pipelined_in_one_process(R, torch_cuda, runs):
+    """DeltaFrame's RCCL path (size exchange, messages posted on a control
+    stream, two frame streams, per-slot buffers) for two ranks in one process,
+    with the exchange replaced by device copies on a side stream under the same
+    stream semantics: every frame of a pose sequence equals rm_render_rgba8's."""
+    torch = torch_cuda
+    from raymarching_amd.frame import DeltaFrame
+    W, H, band = 96, 70, 8
+    side = torch.cuda.Stream()
+    queue = []
+
+    class Work:
+        def __init__(self, entry=None, ev=None):
+            self.entry, self.ev = entry, ev
+
+        def wait(self):
+            ev = self.ev if self.ev is not None else (self.entry or {}).get("done")
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+
+    def fake(fr):
+        def exchange(slot):
+            if fr.rank == 1:
+                fr.size_ev[slot].synchronize()
+                mine = int(fr.size_host[slot][0])
+                entry = {"msg": fr.msg[slot], "size": mine}
+                queue.append(entry)
+                return [0, mine], [Work(entry)]
+            entry = queue.pop(0)
+            if fr.decoded_recorded[slot]:
+                side.wait_event(fr.decoded[slot])
+            with torch.cuda.stream(side):
+                fr.recv[slot][1][: entry["size"]].copy_(entry["msg"][: entry["size"]])
+            done = torch.cuda.Event()
+            done.record(side)
+            entry["done"] = done
+            return [0, entry["size"]], [Work(ev=done)]
+        return exchange
+
+    r1 = rm.Renderer(0)
+    frs = []
+    for rank, rr in ((0, R), (1, r1)):
+        f = DeltaFrame.__new__(DeltaFrame)
+        f._pipelined = lambda: True  # as with the "nccl" backend
+        DeltaFrame.__init__(f, rr, W, H, band, rank, 2, runs=runs)
+        f._sizes_and_messages = fake(f)
+        frs.append(f)
+    assert len(frs[0].streams) == 2
+    poses = ["P0", "P1", "P2", "P3"]
+    refs = []
+    for name in poses:
+        setup(R, "T", POSES[name], 128)
+        R.set_params(count_evals=0)
+        refs.append(R.render_rgba8(W, H).cpu().numpy())
+    got = []
+    for i, name in enumerate(poses):
+        for f, rr in ((frs[1], r1), (frs[0], R)):
+            setup(rr, "T", POSES[name], 128)
+            rr.set_params(count_evals=0)
+            f.submit()
+        if i > 0:
+            torch.cuda.synchronize()
+            got.append(frs[0].frame.cpu().numpy())
+    frs[1].flush()
+    got.append(frs[0].flush().cpu().numpy())
+    torch.cuda.synchronize()
+    for g, ref in zip(got, refs):
+        assert np.array_equal(g, ref)
+    r1.close()

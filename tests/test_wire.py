@@ -1,0 +1,123 @@
+"""The compressed wire of RGBA8 row parts (raymarching_amd/csrc/rm_wire.hip,
+DESIGN.md 4.4): the numpy restatement (tests/wire_codec.py) round-trips on
+CPU; on the GPU the encoder writes the restatement's bytes exactly and the
+decoder rebuilds every part's frame rows bit for bit."""
+import numpy as np
+import pytest
+
+import raymarching_amd as rm
+from tests import wire_codec
+
+
+@pytest.fixture(scope="module")
+def R(torch_cuda):
+    r = rm.Renderer(0)
+    yield r
+    r.close()
+
+
+def _smooth(n, W, seed=0):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:n, 0:W]
+    r = (x * 255 // max(W - 1, 1)).astype(np.uint32)
+    g = ((y * 7 + x // 9) % 256).astype(np.uint32)
+    b = np.where(rng.random((n, W)) < 0.02, rng.integers(0, 256, (n, W)), 128).astype(np.uint32)
+    return r | (g << 8) | (b << 16) | np.uint32(0xFF000000)
+
+
+def _noise(n, W, seed=1):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 2**24, (n, W), dtype=np.uint32) | np.uint32(0xFF000000)
+
+
+@pytest.mark.parametrize("n,W", [(3, 64), (5, 97), (2, 200), (1, 1), (4, 4096)])
+@pytest.mark.parametrize("kind", ["smooth", "noise", "flat"])
+def test_numpy_codec_round_trip(n, W, kind):
+    img = {"smooth": _smooth, "noise": _noise}.get(kind, lambda n, W: np.full((n, W), 0xFF102030, np.uint32))(n, W)
+    msg = wire_codec.encode(img)
+    assert int(np.frombuffer(msg[:8].tobytes(), np.int64)[0]) == msg.size
+    assert msg.size <= rm.wire_capacity(W, n)
+    assert np.array_equal(wire_codec.decode(msg, n, W), img)
+    if kind == "flat":  # 8 bytes per segment plus the tables
+        assert msg.size == 8 + ((4 * n + 7) & ~7) + ((n * ((W + 63) // 64) + 7) & ~7) + 8 * n * ((W + 63) // 64)
+
+
+def test_capacity_and_workspace_sizes():
+    assert rm.wire_capacity(4096, 512) >= 512 * 64 * 25 * 8
+    assert rm.wire_workspace_bytes(4096, 512) == 8 * 25 * 512 * 64 + 4 * 512
+    with pytest.raises(ValueError):
+        rm.wire_capacity(0, 4)
+
+
+def _gpu_encode(R, torch, img):
+    n, W = img.shape
+    rows = torch.from_numpy(img.view(np.int32)).cuda()
+    msg = torch.zeros(rm.wire_capacity(W, n), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(rm.wire_workspace_bytes(W, n), dtype=torch.uint8, device="cuda")
+    size = torch.zeros(1, dtype=torch.int64, device="cuda")
+    R.wire_encode(rows, msg, ws, size)
+    torch.cuda.synchronize()
+    return msg, int(size.item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,W", [(3, 64), (5, 97), (2, 200), (7, 4096)])
+@pytest.mark.parametrize("kind", ["smooth", "noise"])
+def test_gpu_encoder_writes_the_restated_bytes(R, torch_cuda, n, W, kind):
+    torch = torch_cuda
+    img = (_smooth if kind == "smooth" else _noise)(n, W)
+    ref = wire_codec.encode(img)
+    msg, size = _gpu_encode(R, torch, img)
+    assert size == ref.size
+    assert np.array_equal(msg[:size].cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,runs", [(96, 70, (13, 8)), (97, 61, (1, 5, 2)), (4096, 512, (16, 16, 16, 16))])
+def test_gpu_wire_rebuilds_rendered_parts(R, torch_cuda, W, H, runs):
+    """A rendered frame's parts: rank 0's rows scattered, every other part
+    encoded on the GPU and decoded into the frame: equal to rm_render_rgba8."""
+    torch = torch_cuda
+    from raymarching_amd.frame import ShardPlan
+    R.load_scene(rm.SCENE_FILES["T"])
+    R.set_uniform("u_resolution", W, H)
+    p = rm.POSES["P1"]
+    R.set_pose(p["pos"], p["mouse"], p["time"])
+    R.set_params(max_steps=128, count_evals=0)
+    ref = R.render_rgba8(W, H)
+    plan = ShardPlan(W, H, runs[-1], len(runs), runs)
+    frame = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+    sizes = []
+    for s in range(len(runs)):
+        n = plan.count(s)
+        loc = torch.empty((n, W), dtype=torch.int32, device="cuda")
+        R.render_cycle_rows(W, H, plan.cycle, plan.offsets[s], runs[s], 0, n, loc)
+        if s == 0:
+            R.scatter_part_rgba8(W, H, plan.cycle, plan.offsets[s], runs[s], n, loc, frame)
+            continue
+        msg = torch.empty(rm.wire_capacity(W, n), dtype=torch.uint8, device="cuda")
+        ws = torch.empty(rm.wire_workspace_bytes(W, n), dtype=torch.uint8, device="cuda")
+        size = torch.zeros(1, dtype=torch.int64, device="cuda")
+        R.wire_encode(loc, msg, ws, size)
+        # the message as it would arrive: only its `size` bytes
+        got = torch.zeros_like(msg)
+        torch.cuda.synchronize()
+        k = int(size.item())
+        got[:k] = msg[:k]
+        R.wire_decode(W, H, plan.cycle, plan.offsets[s], runs[s], n, got, frame)
+        sizes.append((k, n * W * 3))
+    torch.cuda.synchronize()
+    assert torch.equal(frame, ref)
+    if W == 4096:  # a rendered frame compresses
+        assert all(k * 2 < raw for k, raw in sizes), sizes
+
+
+@pytest.mark.gpu
+def test_gpu_wire_rejects_bad_parts(R, torch_cuda):
+    torch = torch_cuda
+    frame = torch.zeros((8, 64), dtype=torch.int32, device="cuda")
+    msg = torch.zeros(rm.wire_capacity(64, 8), dtype=torch.uint8, device="cuda")
+    with pytest.raises(rm.RmError):
+        R.wire_decode(64, 8, 4, 3, 2, 1, msg, frame)  # offset + run > cycle
+    with pytest.raises(rm.RmError):
+        R.wire_decode(64, 8, 4, 0, 2, 5, msg, frame)  # more rows than the part has
