@@ -67,9 +67,10 @@ def parse():
                          "split that gives rank 0 (which receives every other rank's rows and de-interleaves) "
                          "a longer run per cycle, sized from the timed exchange, and keeps whichever plan ran "
                          "the untimed trial frames faster")
-    ap.add_argument("--wire", default="auto", choices=["auto", "rgb8", "delta"],
-                    help="N > 1: the RGB8 wire (3 B/px), the compressed wire (DeltaFrame: a lossless delta "
-                         "code per 64-pixel row segment), or 'auto': both in the untimed trial, the faster timed")
+    ap.add_argument("--wire", default="rgb8", choices=["auto", "rgb8", "delta"],
+                    help="N > 1: the RGB8 wire (3 B/px, default), the compressed wire (DeltaFrame: a lossless "
+                         "delta code per 64-pixel row segment, 4-5x fewer bytes, DESIGN.md 4.4), or 'auto': both "
+                         "in the untimed trial, the faster timed")
     ap.add_argument("--chunks", type=int, default=None,
                     help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])

@@ -298,7 +298,7 @@ rm_status rm_deinterleave_cycle_rgb8(rm_ctx *ctx, int W, int H, int cycle, int n
  * (cycle, offset, run) into those rows of the W x H RGBA8 frame.
  * rm_scatter_part_rgba8: a part's packed RGBA8 rows into their frame rows
  * (the root's own part).  Capacity/workspace return -1 for bad sizes
- * (W <= 2^18). */
+ * (W <= 2^18; a message holds at most 65535 rows). */
 int64_t rm_wire_capacity(int W, int nrows);
 int64_t rm_wire_workspace_bytes(int W, int nrows);
 rm_status rm_wire_encode(rm_ctx *ctx, int W, int nrows, const uint32_t *rows, uint8_t *msg, void *workspace,
@@ -307,6 +307,11 @@ rm_status rm_wire_decode(rm_ctx *ctx, int W, int H, int cycle, int offset, int r
                          uint32_t *frame);
 rm_status rm_scatter_part_rgba8(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int nrows,
                                 const uint32_t *rows, uint32_t *frame);
+/* rm_wire_decode for nparts (<= 64) messages in one launch: part i holds
+ * nrows[i] rows of (cycle, offsets[i], runs[i]); msgs is a host array of
+ * device pointers. */
+rm_status rm_wire_decode_parts(rm_ctx *ctx, int W, int H, int cycle, int nparts, const int *offsets, const int *runs,
+                               const int *nrows, const uint8_t *const *msgs, uint32_t *frame);
 
 /* ---- Multi-GPU: row-sharded frames over RCCL ----
  * The reference renders one frame on one GPU (main.cpp:196-207); here a frame's

@@ -28,7 +28,7 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_set_tile_order", "rm_tile_grid", "rm_comm_info", "rm_abi_version", "rm_cycle_rows",
            "rm_render_cycle_rows", "rm_render_cycle_rows_rgba8", "rm_deinterleave_cycle_rgb8",
            "rm_render_sharded_runs", "rm_render_sharded_runs_all", "rm_wire_capacity", "rm_wire_workspace_bytes",
-           "rm_wire_encode", "rm_wire_decode", "rm_scatter_part_rgba8")
+           "rm_wire_encode", "rm_wire_decode", "rm_scatter_part_rgba8", "rm_wire_decode_parts")
 
 # include/rm.h RM_ABI_VERSION: the struct layouts below
 ABI_VERSION = 3
@@ -144,6 +144,7 @@ def lib() -> ctypes.CDLL:
         "rm_wire_encode": ([vp, c.c_int, c.c_int, vp, vp, vp, vp], c.c_int),
         "rm_wire_decode": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_scatter_part_rgba8": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp], c.c_int),
+        "rm_wire_decode_parts": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp, vp, vp, vp], c.c_int),
         "rm_render_sharded_runs": ([vp, c.c_int, c.c_int, vp, vp, c.POINTER(RmStats)], c.c_int),
         "rm_render_sharded_runs_all": ([c.POINTER(vp), c.c_int, c.c_int, c.c_int, vp, vp, c.POINTER(RmStats)],
                                        c.c_int),

@@ -251,6 +251,17 @@ class Renderer:
                                    self._ptr(msg), self._ptr(frame)), self._ctx)
         return frame
 
+    def wire_decode_parts(self, W, H, cycle, offsets, runs, nrows, msgs, frame):
+        """rm_wire_decode_parts: several parts' messages (uint8 device tensors)
+        into the int32 [H, W] frame in one launch."""
+        _check_out(frame, H * W)
+        n = len(msgs)
+        check(lib().rm_wire_decode_parts(self._ctx, int(W), int(H), int(cycle), n, (ctypes.c_int * n)(*offsets),
+                                         (ctypes.c_int * n)(*runs), (ctypes.c_int * n)(*nrows),
+                                         (ctypes.c_void_p * n)(*[m.data_ptr() for m in msgs]), self._ptr(frame)),
+              self._ctx)
+        return frame
+
     def scatter_part_rgba8(self, W, H, cycle, offset, run, nrows, rows, frame):
         """A part's packed RGBA8 rows (int32 [nrows, W]) into their frame rows."""
         _check_out(frame, H * W)

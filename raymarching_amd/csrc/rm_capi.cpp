@@ -969,7 +969,7 @@ int64_t rm_wire_workspace_bytes(int W, int nrows) {
 rm_status rm_wire_encode(rm_ctx *ctx, int W, int nrows, const uint32_t *rows, uint8_t *msg, void *workspace,
                          int64_t *size_out) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
-    if (W <= 0 || W > (1 << 18) || nrows < 0 || !msg || !workspace || (nrows > 0 && !rows))
+    if (W <= 0 || W > (1 << 18) || nrows < 0 || nrows > 65535 || !msg || !workspace || (nrows > 0 && !rows))
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_encode: bad arguments");
     if (!is_device_ptr(msg) || !is_device_ptr(workspace) || (nrows > 0 && !is_device_ptr(rows)) ||
         (size_out && !is_device_ptr(size_out)))
@@ -985,13 +985,37 @@ rm_status rm_wire_decode(rm_ctx *ctx, int W, int H, int cycle, int offset, int r
                          uint32_t *frame) {
     RowPart p;
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
-    if (W <= 0 || W > (1 << 18) || H <= 0 || !cycle_part(cycle, offset, run, p) || nrows < 0 ||
+    if (W <= 0 || W > (1 << 18) || H <= 0 || !cycle_part(cycle, offset, run, p) || nrows < 0 || nrows > 65535 ||
         nrows > rows_of_part(H, p) || !msg || !frame)
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_decode: bad arguments");
     if (!is_device_ptr(msg) || !is_device_ptr(frame))
         return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_decode: device pointers required");
     RM_HIP(hipSetDevice(ctx->device));
     hipError_t e = rm::launch_wire_decode(msg, nrows, W, cycle, offset, run, frame, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "wire decode launch");
+    return mark_done(ctx);
+}
+
+rm_status rm_wire_decode_parts(rm_ctx *ctx, int W, int H, int cycle, int nparts, const int *offsets, const int *runs,
+                               const int *nrows, const uint8_t *const *msgs, uint32_t *frame) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (W <= 0 || W > (1 << 18) || H <= 0 || nparts < 0 || nparts > rm::kMaxWireParts || !frame ||
+        (nparts > 0 && (!offsets || !runs || !nrows || !msgs)))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_decode_parts: bad arguments");
+    rm::WireParts parts;
+    std::memset(&parts, 0, sizeof(parts));
+    parts.n = nparts;
+    parts.cycle = cycle;
+    for (int i = 0; i < nparts; i++) {
+        RowPart p;
+        if (!cycle_part(cycle, offsets[i], runs[i], p) || nrows[i] < 0 || nrows[i] > 65535 ||
+            nrows[i] > rows_of_part(H, p) || !msgs[i] || !is_device_ptr(msgs[i]))
+            return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_decode_parts: bad part");
+        parts.part[i] = rm::WirePart{msgs[i], nrows[i], offsets[i], runs[i]};
+    }
+    if (!is_device_ptr(frame)) return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_wire_decode_parts: device frame required");
+    RM_HIP(hipSetDevice(ctx->device));
+    hipError_t e = rm::launch_wire_decode_parts(parts, W, frame, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "wire decode launch");
     return mark_done(ctx);
 }

@@ -56,6 +56,16 @@ hipError_t launch_wire_encode(const uint32_t* rows, int W, int n, uint8_t* msg, 
                               long long* size_out, hipStream_t s);
 hipError_t launch_wire_decode(const uint8_t* msg, int n, int W, int cycle, int offset, int run, uint32_t* frame,
                               hipStream_t s);
+constexpr int kMaxWireParts = 64;
+struct WirePart {
+    const uint8_t* msg;
+    int nrows, offset, run;
+};
+struct WireParts {
+    int n, cycle;
+    WirePart part[kMaxWireParts];
+};
+hipError_t launch_wire_decode_parts(const WireParts& parts, int W, uint32_t* frame, hipStream_t s);
 hipError_t launch_scatter_part(const uint32_t* rows, int n, int W, int cycle, int offset, int run, uint32_t* frame,
                                hipStream_t s);
 

@@ -19,8 +19,9 @@
 //   then payload      uint64 words: per row, per segment: header, planes
 // The encoder writes every segment's words into a fixed slot of a workspace
 // (25 words: the widest segment), then scans the rows and compacts the slots
-// into the message; the decoder scans a row's segment sizes in LDS and
-// rebuilds each segment with a wave-wide prefix sum of the differences.
+// into the message; the decoder gives every segment a wave, which sums the
+// row's earlier segment sizes and rebuilds its 64 pixels with a wave-wide
+// prefix sum of the differences.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -118,88 +119,114 @@ __global__ __launch_bounds__(1024) void rm_wire_row_scan(const uint32_t* __restr
     }
 }
 
-// exclusive scan of a row's S segment word counts into sh[0..S) (S <= 4096),
-// the row's total returned; 256 threads
-__device__ __forceinline__ void row_seg_offsets(const uint8_t* counts, int S, uint32_t* sh) {
-    const int t = threadIdx.x;
-    for (int k = t; k < S; k += 256) sh[k] = counts[k];
-    __syncthreads();
-    if (t < 64) {  // one wave: sequential chunks of the scan, lane-parallel within 64
-        uint32_t carry = 0;
-        for (int k0 = 0; k0 < S; k0 += 64) {
-            const int k = k0 + t;
-            uint32_t v = k < S ? sh[k] : 0u, inc = v;
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(inc, o, 64);
-                if (t >= o) inc += u;
-            }
-            if (k < S) sh[k] = carry + inc - v;
-            carry += __shfl(inc, 63, 64);
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// words of a row's segments before segment k (one wave, wave-uniform result)
+__device__ __forceinline__ uint32_t seg_offset(const uint8_t* __restrict__ counts, int k, int l) {
+    uint32_t acc = 0;
+    for (int c0 = 0; c0 < k; c0 += 64) {
+        const int kk = c0 + l;
+        acc += wave_sum(kk < k ? (uint32_t)counts[kk] : 0u);
+    }
+    return acc;
+}
+
+// E3: one wave per segment (grid S x n): its slot's words into the payload
+__global__ __launch_bounds__(64) void rm_wire_compact(const uint64_t* __restrict__ slots, int n,
+                                                      uint8_t* __restrict__ msg) {
+    const int k = blockIdx.x, j = blockIdx.y, l = threadIdx.x, S = gridDim.x;
+    const size_t hb = wire_header_bytes(n, S);
+    const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
+    const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
+    const int cnt = counts[k];
+    if (l < cnt)
+        reinterpret_cast<uint64_t*>(msg + hb)[off + l] = slots[((size_t)j * S + k) * kSegWords + l];
+}
+
+// D: one wave per segment of a part's packed row j (grid S x n): rebuilt into
+// frame row y(j) (the part's rows: (y mod cycle) - offset in [0, run))
+__global__ __launch_bounds__(64) void rm_wire_decode(const uint8_t* __restrict__ msg, int n, int W, int cycle,
+                                                     int offset, int run, uint32_t* __restrict__ frame) {
+    const int k = blockIdx.x, j = blockIdx.y, l = threadIdx.x, S = gridDim.x;
+    const size_t hb = wire_header_bytes(n, S);
+    const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
+    const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
+    const int cnt = counts[k];
+    const uint64_t* sw = reinterpret_cast<const uint64_t*>(msg + hb) + off;
+    const uint64_t mine = l < cnt ? sw[l] : 0ull;  // lane 0: header, lane q + 1: plane q
+    const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
+    const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_lo);
+    const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_hi);
+    const int b[3] = {(int)((h_lo >> 24) & 15u), (int)(h_lo >> 28), (int)(h_hi & 15u)};
+    // this lane's bit of a plane word: from the low half for lanes 0-31, the high half for 32-63
+    const uint32_t sh = (uint32_t)(l & 31);
+    const bool hi_half = l >= 32;
+    uint32_t px = 0;
+    int q = 1;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        uint32_t z = 0;
+        for (int i = 0; i < b[c]; i++, q++) {
+            const uint32_t w = hi_half ? (uint32_t)__builtin_amdgcn_readlane((int)m_hi, q)
+                                       : (uint32_t)__builtin_amdgcn_readlane((int)m_lo, q);
+            z |= ((w >> sh) & 1u) << i;
         }
+        int d = l == 0 ? (int)((h_lo >> (8 * c)) & 255u) : unzigzag8(z);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive prefix sum over the lanes
+            const int u = __shfl_up(d, o, 64);
+            if (l >= o) d += u;
+        }
+        px |= (uint32_t)(d & 255) << (8 * c);
     }
-    __syncthreads();
-}
-
-// E3: one workgroup per row: the row's slots, compacted into the payload
-__global__ __launch_bounds__(256) void rm_wire_compact(const uint64_t* __restrict__ slots, int n, int S,
-                                                       uint8_t* __restrict__ msg) {
-    extern __shared__ uint32_t seg_off[];
-    const int j = blockIdx.x;
-    const size_t hb = wire_header_bytes(n, S);
-    const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
-    row_seg_offsets(counts, S, seg_off);
-    const uint32_t base = reinterpret_cast<const uint32_t*>(msg + 8)[j];
-    uint64_t* payload = reinterpret_cast<uint64_t*>(msg + hb) + base;
-    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-    for (int k = wv; k < S; k += 4) {
-        const int cnt = counts[k];
-        if (l < cnt) payload[seg_off[k] + l] = slots[((size_t)j * S + k) * kSegWords + l];
-    }
-}
-
-// D: one workgroup per packed row of a part: its segments rebuilt into frame
-// row y(j) (the part's rows: (y mod cycle) - offset in [0, run))
-__global__ __launch_bounds__(256) void rm_wire_decode(const uint8_t* __restrict__ msg, int n, int W, int cycle,
-                                                      int offset, int run, uint32_t* __restrict__ frame) {
-    extern __shared__ uint32_t seg_off[];
-    const int j = blockIdx.x, S = (W + 63) / 64;
-    const size_t hb = wire_header_bytes(n, S);
-    const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
-    row_seg_offsets(counts, S, seg_off);
-    const uint32_t base = reinterpret_cast<const uint32_t*>(msg + 8)[j];
-    const uint64_t* payload = reinterpret_cast<const uint64_t*>(msg + hb) + base;
     const int c0 = j / run, y = c0 * cycle + offset + (j - c0 * run);
-    uint32_t* dst = frame + (size_t)y * W;
-    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-    for (int k = wv; k < S; k += 4) {
-        const uint64_t* sw = payload + seg_off[k];
+    const int x = k * 64 + l;
+    if (x < W) frame[(size_t)y * W + x] = px | 0xFF000000u;
+}
+
+// D for several parts in one launch (grid S x max rows x parts)
+__global__ __launch_bounds__(64) void rm_wire_decode_parts(WireParts parts, int W, uint32_t* __restrict__ frame) {
+    const WirePart& P = parts.part[blockIdx.z];
+    const int k = blockIdx.x, l = threadIdx.x, S = gridDim.x, n = P.nrows;
+    const size_t hb = wire_header_bytes(n, S);
+    for (int j = blockIdx.y; j < n; j += gridDim.y) {
+        const uint8_t* msg = P.msg;
+        const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
+        const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
         const int cnt = counts[k];
-        const uint64_t mine = l < cnt ? sw[l] : 0ull;  // lane 0: header, lane q + 1: plane q
-        const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mine);
-        const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mine >> 32));
+        const uint64_t* sw = reinterpret_cast<const uint64_t*>(msg + hb) + off;
+        const uint64_t mine = l < cnt ? sw[l] : 0ull;
+        const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
+        const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_lo);
+        const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_hi);
         const int b[3] = {(int)((h_lo >> 24) & 15u), (int)(h_lo >> 28), (int)(h_hi & 15u)};
+        const uint32_t sh = (uint32_t)(l & 31);
+        const bool hi_half = l >= 32;
         uint32_t px = 0;
         int q = 1;
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             uint32_t z = 0;
             for (int i = 0; i < b[c]; i++, q++) {
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, q);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), q);
-                const uint32_t bit = l < 32 ? (lo >> l) & 1u : (hi >> (l - 32)) & 1u;
-                z |= bit << i;
+                const uint32_t w = hi_half ? (uint32_t)__builtin_amdgcn_readlane((int)m_hi, q)
+                                           : (uint32_t)__builtin_amdgcn_readlane((int)m_lo, q);
+                z |= ((w >> sh) & 1u) << i;
             }
             int d = l == 0 ? (int)((h_lo >> (8 * c)) & 255u) : unzigzag8(z);
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {  // inclusive prefix sum over the lanes
+            for (int o = 1; o < 64; o <<= 1) {
                 const int u = __shfl_up(d, o, 64);
                 if (l >= o) d += u;
             }
             px |= (uint32_t)(d & 255) << (8 * c);
         }
+        const int c0 = j / P.run, y = c0 * parts.cycle + P.offset + (j - c0 * P.run);
         const int x = k * 64 + l;
-        if (x < W) dst[x] = px | 0xFF000000u;
+        if (x < W) frame[(size_t)y * W + x] = px | 0xFF000000u;
     }
 }
 
@@ -238,7 +265,7 @@ hipError_t launch_wire_encode(const uint32_t* rows, int W, int n, uint8_t* msg, 
     }
     hipLaunchKernelGGL(rm_wire_row_scan, dim3(1), dim3(1024), 0, s, row_words, n, S, msg, size_out);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (n > 0) hipLaunchKernelGGL(rm_wire_compact, dim3(n), dim3(256), (size_t)4 * S, s, slots, n, S, msg);
+    if (n > 0) hipLaunchKernelGGL(rm_wire_compact, dim3(S, n), dim3(64), 0, s, slots, n, msg);
     return hipGetLastError();
 }
 
@@ -246,7 +273,17 @@ hipError_t launch_wire_decode(const uint8_t* msg, int n, int W, int cycle, int o
                               hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int S = (W + 63) / 64;
-    hipLaunchKernelGGL(rm_wire_decode, dim3(n), dim3(256), (size_t)4 * S, s, msg, n, W, cycle, offset, run, frame);
+    hipLaunchKernelGGL(rm_wire_decode, dim3(S, n), dim3(64), 0, s, msg, n, W, cycle, offset, run, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_wire_decode_parts(const WireParts& parts, int W, uint32_t* frame, hipStream_t s) {
+    int rows = 0;
+    for (int i = 0; i < parts.n; i++) rows = parts.part[i].nrows > rows ? parts.part[i].nrows : rows;
+    if (parts.n <= 0 || rows <= 0) return hipSuccess;
+    const int S = (W + 63) / 64;
+    hipLaunchKernelGGL(rm_wire_decode_parts, dim3(S, rows < 65535 ? rows : 65535, parts.n), dim3(64), 0, s, parts,
+                       W, frame);
     return hipGetLastError();
 }
 

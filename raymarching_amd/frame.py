@@ -581,6 +581,35 @@ class DeltaFrame(DistributedFrame):
         self.k = 0
         self.pending = None
         self.last_sizes = [0] * world
+        # the per-frame native calls with their arguments built once (a frame
+        # at N = 8 is ~0.1 ms: Python-side argument checks per call would cost
+        # as much as the GPU work)
+        import ctypes
+
+        from ._lib import lib
+        self._L = lib()
+        if rank == 0:
+            qs = list(range(1, world))
+            self._dec = [((ctypes.c_int * len(qs))(*[p.offsets[q] for q in qs]),
+                          (ctypes.c_int * len(qs))(*[p.part_runs[q] for q in qs]),
+                          (ctypes.c_int * len(qs))(*[p.count(q) for q in qs]),
+                          (ctypes.c_void_p * len(qs))(*[self.recv[s_][q].data_ptr() for q in qs]))
+                         for s_ in range(nbuf)]
+
+    def _call(self, rc):
+        from ._lib import check
+        check(rc, self.r._ctx)
+
+    def _encode(self, slot):
+        self._call(self._L.rm_wire_encode(self.r._ctx, self.plan.W, self.nmine, self.locals[slot].data_ptr(),
+                                          self.msg[slot].data_ptr(), self.ws[slot].data_ptr(),
+                                          self.size_dev[slot].data_ptr()))
+
+    def _scatter(self, slot):
+        p = self.plan
+        self._call(self._L.rm_scatter_part_rgba8(self.r._ctx, p.W, p.H, p.cycle, p.offsets[0], p.part_runs[0],
+                                                 self.nmine, self.locals[slot].data_ptr(),
+                                                 self.frames[slot].data_ptr()))
 
     def _produce(self, slot, st, events=None):
         """Render this rank's rows into slot `slot` on stream st, then (root)
@@ -599,10 +628,9 @@ class DeltaFrame(DistributedFrame):
             if events is not None:
                 events[1].record()
             if self.rank == 0:
-                self.r.scatter_part_rgba8(p.W, p.H, p.cycle, p.offsets[0], p.part_runs[0], self.nmine,
-                                          self.locals[slot], self.frames[slot])
+                self._scatter(slot)
             else:
-                self.r.wire_encode(self.locals[slot], self.msg[slot], self.ws[slot], self.size_dev[slot])
+                self._encode(slot)
                 self.size_host[slot].copy_(self.size_dev[slot], non_blocking=True)
                 self.size_ev[slot].record(st)
         self.r.set_stream(self.caller)
@@ -646,9 +674,8 @@ class DeltaFrame(DistributedFrame):
 
     def _decode(self, slot, st):
         p = self.plan
-        for q in range(1, self.world):
-            self.r.wire_decode(p.W, p.H, p.cycle, p.offsets[q], p.part_runs[q], p.count(q), self.recv[slot][q],
-                               self.frames[slot])
+        self._call(self._L.rm_wire_decode_parts(self.r._ctx, p.W, p.H, p.cycle, self.world - 1, *self._dec[slot],
+                                                self.frames[slot].data_ptr()))
 
     def _exchange(self, slot, st):
         """Sizes, messages, and on rank 0 the decodes into its frame on st."""
@@ -730,10 +757,9 @@ class DeltaFrame(DistributedFrame):
                 self._render_into(self.locals[slot], 0, self.nmine)
             ev[1].record(st)
             if self.rank == 0:
-                self.r.scatter_part_rgba8(p.W, p.H, p.cycle, p.offsets[0], p.part_runs[0], self.nmine,
-                                          self.locals[slot], self.frames[slot])
+                self._scatter(slot)
             else:
-                self.r.wire_encode(self.locals[slot], self.msg[slot], self.ws[slot], self.size_dev[slot])
+                self._encode(slot)
                 self.size_host[slot].copy_(self.size_dev[slot], non_blocking=True)
                 self.size_ev[slot].record(st)
             ev[2].record(st)
