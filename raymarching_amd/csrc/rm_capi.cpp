@@ -52,12 +52,15 @@ struct rm_ctx {
     };
     static constexpr int kPersistBlocks = 4;
     std::vector<PersistBlock> persist;
-    // work this context enqueued: `done` is recorded after each call that
-    // enqueues on `stream`; when the stream changes, the previous one's event
-    // is kept in `retired` until it completes (rm_destroy waits for these and
-    // the side stream instead of the whole device)
+    // work this context enqueued: `dirty` is set by each call that enqueues
+    // on `stream`; `done` is recorded on the stream only when the context
+    // leaves it (rm_set_stream) or is destroyed -- an event recorded after
+    // every launch cost a ~11 us gap between consecutive frames on the stream
+    // (DESIGN.md 2.14).  A left stream's event stays in `retired` until it
+    // completes (rm_destroy waits for these and the side stream, not the
+    // whole device).
     hipEvent_t done = nullptr;
-    bool done_recorded = false;
+    bool dirty = false;
     std::vector<hipEvent_t> retired;
     float sample_part = 1.0f;  // u_sample_part, u_seed1, u_seed2: read by rm_render_accumulate*
     float seed1[2] = {0.0f, 0.0f}, seed2[2] = {0.0f, 0.0f};
@@ -88,7 +91,8 @@ struct rm_ctx {
         uint64_t k = 0;            // launches so far
         uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256])
         hipEvent_t rendered = nullptr, sorted[2] = {nullptr, nullptr};
-        hipEvent_t last = nullptr;  // recorded after every launch that reads or writes buf
+        hipEvent_t last = nullptr;  // after the last launch that read or wrote buf: recorded on `stream`
+        bool dirty = false;         // when the context leaves the stream or the entry is released
         uint64_t used = 0;
     };
     Sched sched[8];
@@ -114,11 +118,22 @@ rm_status hip_fail(rm_ctx *c, hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
     } while (0)
 
-// Record that the context enqueued work on its stream (rm_ctx::done).
+// Note that the context enqueued work on its stream (rm_ctx::dirty).
 rm_status mark_done(rm_ctx *ctx) {
-    RM_HIP(hipEventRecord(ctx->done, ctx->stream));
-    ctx->done_recorded = true;
+    ctx->dirty = true;
     return RM_OK;
+}
+
+// Record the adaptive-order entries' `last` events still owed on the ctx
+// stream (before the context leaves it, or releases an entry of it).
+hipError_t record_sched_last(rm_ctx *ctx) {
+    for (rm_ctx::Sched &e : ctx->sched)
+        if (e.buf && e.dirty && e.stream == ctx->stream) {
+            hipError_t r = hipEventRecord(e.last, ctx->stream);
+            if (r != hipSuccess) return r;
+            e.dirty = false;
+        }
+    return hipSuccess;
 }
 
 // The KERNEL_PERSIST counter block of the ctx stream (rm_ctx::PersistBlock).
@@ -428,7 +443,8 @@ int pick_kernel(const rm_ctx *c) {
 hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
     hipError_t r = hipSuccess;
     if (e.buf) {
-        if (e.last) r = hipEventSynchronize(e.last);
+        if (e.dirty && e.stream == ctx->stream) r = hipEventRecord(e.last, ctx->stream);
+        if (r == hipSuccess && e.last) r = hipEventSynchronize(e.last);
         if (r == hipSuccess && ctx->side) r = hipStreamSynchronize(ctx->side);
         (void)hipFree(e.buf);
     }
@@ -545,7 +561,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
         RM_HIP(hipEventRecord(sc->sorted[slot], ctx->side));
     }
     if (sc) {
-        RM_HIP(hipEventRecord(sc->last, ctx->stream));
+        sc->dirty = true;  // (its `last` event is recorded when the context leaves the stream)
         if (!cnt) sc->k++;
     }
     rm_status ms_st = mark_done(ctx);
@@ -712,7 +728,9 @@ rm_status rm_destroy(rm_ctx *ctx) {
     // nothing this context enqueued still runs: its own events (the streams
     // may be the caller's and gone by now) and its side stream; other work on
     // the device is not waited for
-    if (ctx->done && ctx->done_recorded) (void)hipEventSynchronize(ctx->done);
+    (void)record_sched_last(ctx);
+    if (ctx->done && ctx->dirty && hipEventRecord(ctx->done, ctx->stream) == hipSuccess)
+        (void)hipEventSynchronize(ctx->done);
     for (hipEvent_t ev : ctx->retired) {
         (void)hipEventSynchronize(ev);
         (void)hipEventDestroy(ev);
@@ -720,7 +738,7 @@ rm_status rm_destroy(rm_ctx *ctx) {
     for (auto &b : ctx->persist)
         if (b.last) (void)hipEventSynchronize(b.last);
     for (rm_ctx::Sched &e : ctx->sched)
-        if (e.last) (void)hipEventSynchronize(e.last);
+        if (e.buf && e.last) (void)hipEventSynchronize(e.last);
     if (ctx->side) (void)hipStreamSynchronize(ctx->side);
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
@@ -835,10 +853,13 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *p) {
 rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (s != ctx->stream && ctx->done_recorded) {
-        // keep the old stream's last-work event until it completes; reuse a
-        // completed one for the new stream (no host wait here)
+    if (s != ctx->stream && ctx->dirty) {
+        // the old stream's last-work events, recorded now (it may be gone by
+        // the time they are waited for); `done` is kept until it completes,
+        // a completed one is reused for the new stream (no host wait here)
         RM_HIP(hipSetDevice(ctx->device));
+        RM_HIP(record_sched_last(ctx));
+        RM_HIP(hipEventRecord(ctx->done, ctx->stream));
         hipEvent_t next = nullptr;
         for (size_t i = 0; i < ctx->retired.size(); i++)
             if (hipEventQuery(ctx->retired[i]) == hipSuccess) {
@@ -850,7 +871,7 @@ rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
         if (!next) RM_HIP(hipEventCreateWithFlags(&next, hipEventDisableTiming));
         ctx->retired.push_back(ctx->done);
         ctx->done = next;
-        ctx->done_recorded = false;
+        ctx->dirty = false;
     }
     ctx->stream = s;
     return RM_OK;
