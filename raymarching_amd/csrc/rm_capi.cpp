@@ -57,7 +57,7 @@ struct rm_ctx {
     // leaves it (rm_set_stream) or is destroyed -- an event recorded after
     // every launch cost a ~11 us gap between consecutive frames on the stream
     // (DESIGN.md 2.14).  A left stream's event stays in `retired` until it
-    // completes (rm_destroy waits for these and the side stream, not the
+    // completes (rm_destroy waits for these, not the
     // whole device).
     hipEvent_t done = nullptr;
     bool dirty = false;
@@ -80,24 +80,23 @@ struct rm_ctx {
     // stream, the tile durations of the last launch and the order they give
     // Every sched_period()-th launch of a geometry (L_s = s * period, s = 0, 1,
     // ...) writes its tile durations into cost[s & 1]; sort s of those
-    // durations runs on the context's side stream, overlapping the next
-    // launch, and writes order[s & 1], which launches L_s + 2 .. L_{s+1} + 1
-    // dispatch (the first of them waits for the sort's event).  The other
-    // launches write no durations.
+    // durations runs right after it on the same stream and writes order[s & 1],
+    // which launches L_s + 1 .. L_{s+1} dispatch.  The other launches write no
+    // durations.  (Round 2-4 sorted on a side stream, overlapping the next
+    // launch: its kernels only got CUs as that launch drained, and the launch
+    // after it waited ~45 us for them)
     struct Sched {
         uint64_t key = 0;
         hipStream_t stream = nullptr;
         int n = 0, gx = 0;         // tiles, tile-grid width
         uint64_t k = 0;            // launches so far
         uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256])
-        hipEvent_t rendered = nullptr, sorted[2] = {nullptr, nullptr};
         hipEvent_t last = nullptr;  // after the last launch that read or wrote buf: recorded on `stream`
         bool dirty = false;         // when the context leaves the stream or the entry is released
         uint64_t used = 0;
     };
     Sched sched[8];
     uint64_t sched_clock = 0;
-    hipStream_t side = nullptr;  // the dispatch-order sorts
 };
 
 namespace {
@@ -445,11 +444,9 @@ hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
     if (e.buf) {
         if (e.dirty && e.stream == ctx->stream) r = hipEventRecord(e.last, ctx->stream);
         if (r == hipSuccess && e.last) r = hipEventSynchronize(e.last);
-        if (r == hipSuccess && ctx->side) r = hipStreamSynchronize(ctx->side);
         (void)hipFree(e.buf);
     }
-    for (hipEvent_t ev : {e.rendered, e.sorted[0], e.sorted[1], e.last})
-        if (ev) (void)hipEventDestroy(ev);
+    if (e.last) (void)hipEventDestroy(e.last);
     e = rm_ctx::Sched();
     return r;
 }
@@ -477,12 +474,10 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, const RowPart &part, int ro
         if (e.used < lru->used) lru = &e;
     }
     hipError_t e = hipSuccess;
-    if (!ctx->side) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = sched_release(ctx, *lru);
+    e = sched_release(ctx, *lru);
     if (e == hipSuccess) e = hipMalloc(&lru->buf, ((size_t)4 * n + 1024) * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 4 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->side);
-    for (hipEvent_t *ev : {&lru->rendered, &lru->sorted[0], &lru->sorted[1], &lru->last})
-        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 4 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->stream);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&lru->last, hipEventDisableTiming);
     if (e != hipSuccess) {
         (void)sched_release(ctx, *lru);
         st = hip_fail(ctx, e, "schedule buffers");
@@ -525,9 +520,8 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
             // does not advance the geometry's launch count
             if (k % P == 0 && !(ctx->params.count_evals != 0 || evmap))
                 F.tile_cost = sc->buf + ((k / P) & 1) * sc->n;  // sort k / P reads them
-            if (k >= 2) {  // the newest order whose sort had a launch to overlap
-                const uint64_t s = (k - 2) / P;
-                if (k - 2 == s * P) RM_HIP(hipStreamWaitEvent(ctx->stream, sc->sorted[s & 1], 0));
+            if (k >= 1) {  // the newest sort's order (it ran right after launch s * P, same stream)
+                const uint64_t s = (k - 1) / P;
                 F.tile_order = sc->buf + (2 + (s & 1)) * sc->n;
             }
         }
@@ -549,16 +543,12 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
     if (pb) RM_HIP(hipEventRecord(pb->last, ctx->stream));
-    if (sc && F.tile_cost) {  // sort this launch's durations on the side stream, overlapping the next launch
+    if (sc && F.tile_cost) {  // sort this launch's durations, on its stream right after it
         const size_t slot = (sc->k / (uint64_t)sched_period()) & 1;
         uint32_t *h = sc->buf + 4 * (size_t)sc->n;
-        RM_HIP(hipEventRecord(sc->rendered, ctx->stream));
-        RM_HIP(hipStreamWaitEvent(ctx->side, sc->rendered, 0));
         e = rm::launch_tile_order(sc->buf + slot * sc->n, sc->n, sc->gx, sched_dilate(), sc->buf + (2 + slot) * sc->n,
-                                  h + 512 * slot,
-                                  h + 512 * (1 - slot), ctx->side);
+                                  h + 512 * slot, h + 512 * (1 - slot), ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
-        RM_HIP(hipEventRecord(sc->sorted[slot], ctx->side));
     }
     if (sc) {
         sc->dirty = true;  // (its `last` event is recorded when the context leaves the stream)
@@ -726,8 +716,8 @@ rm_status rm_destroy(rm_ctx *ctx) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     (void)hipSetDevice(ctx->device);
     // nothing this context enqueued still runs: its own events (the streams
-    // may be the caller's and gone by now) and its side stream; other work on
-    // the device is not waited for
+    // it left may be the caller's and gone by now); other work on the device
+    // is not waited for
     (void)record_sched_last(ctx);
     if (ctx->done && ctx->dirty && hipEventRecord(ctx->done, ctx->stream) == hipSuccess)
         (void)hipEventSynchronize(ctx->done);
@@ -739,7 +729,6 @@ rm_status rm_destroy(rm_ctx *ctx) {
         if (b.last) (void)hipEventSynchronize(b.last);
     for (rm_ctx::Sched &e : ctx->sched)
         if (e.buf && e.last) (void)hipEventSynchronize(e.last);
-    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
     for (auto &b : ctx->persist) {
@@ -750,7 +739,6 @@ rm_status rm_destroy(rm_ctx *ctx) {
     if (ctx->mips) (void)hipFree(ctx->mips);
     if (ctx->tile_order) (void)hipFree(ctx->tile_order);
     for (rm_ctx::Sched &e : ctx->sched) (void)sched_release(ctx, e);
-    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->done) (void)hipEventDestroy(ctx->done);
