@@ -90,7 +90,7 @@ struct rm_ctx {
         hipStream_t stream = nullptr;
         int n = 0, gx = 0;         // tiles, tile-grid width
         uint64_t k = 0;            // launches so far
-        uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256])
+        uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256]) | bucket u8[n]
         hipEvent_t last = nullptr;  // after the last launch that read or wrote buf: recorded on `stream`
         bool dirty = false;         // when the context leaves the stream or the entry is released
         uint64_t used = 0;
@@ -475,7 +475,8 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, const RowPart &part, int ro
     }
     hipError_t e = hipSuccess;
     e = sched_release(ctx, *lru);
-    if (e == hipSuccess) e = hipMalloc(&lru->buf, ((size_t)4 * n + 1024) * sizeof(uint32_t));
+    // cost[2][n] | order[2][n] | 2 x (hist | cursor) | bucket bytes[n]
+    if (e == hipSuccess) e = hipMalloc(&lru->buf, ((size_t)4 * n + 1024 + ((size_t)n + 3) / 4) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 4 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->stream);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&lru->last, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -547,7 +548,8 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
         const size_t slot = (sc->k / (uint64_t)sched_period()) & 1;
         uint32_t *h = sc->buf + 4 * (size_t)sc->n;
         e = rm::launch_tile_order(sc->buf + slot * sc->n, sc->n, sc->gx, sched_dilate(), sc->buf + (2 + slot) * sc->n,
-                                  h + 512 * slot, h + 512 * (1 - slot), ctx->stream);
+                                  h + 512 * slot, h + 512 * (1 - slot), reinterpret_cast<uint8_t *>(h + 1024),
+                                  ctx->stream);
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
     }
     if (sc) {

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void rm_deinterleave_cycle_rgb8(const uint8_t*
 // scan of the histogram) + the block's reservation in the bucket (cursor) +
 // the tile's rank in the block, and clears the other parity's histogram and
 // cursors (`next`) for the following sort (no memset on the stream).  The
-// context runs both on a side stream, overlapping the next frame's render.
+// context runs both on the frame's stream right after the measuring launch.
 // The sort key of tile i: its duration, or with a dilation radius r > 0 the
 // longest duration among the tiles within r of it on the gx-wide tile grid
 // (an order that stays right while the costly regions move a few tiles
@@ -151,18 +151,42 @@ __device__ __forceinline__ uint32_t tile_key(const uint32_t* __restrict__ cost, 
     return m;
 }
 
+// tile_key for a compile-time radius: every load in flight at once (the
+// run-time loop waited on each of its 25 loads in turn: 17 us per sort)
+template <int R>
+__device__ __forceinline__ uint32_t tile_key_r(const uint32_t* __restrict__ cost, int i, int n, int gx) {
+    const int x = i % gx, y = i / gx;
+    uint32_t m = 0;
+#pragma unroll
+    for (int dy = -R; dy <= R; dy++)
+#pragma unroll
+        for (int dx = -R; dx <= R; dx++) {
+            const int yy = y + dy, xx = x + dx, j = yy * gx + xx;
+            const bool in = yy >= 0 && xx >= 0 && xx < gx && j < n;
+            const uint32_t v = cost[in ? j : i];
+            m = max(m, v);
+        }
+    return m;
+}
+
+// one tile per thread: its bucket (kept for the scatter: the dilated key reads
+// (2r + 1)^2 durations, formed once) and the block's histogram
 __global__ __launch_bounds__(256) void rm_sched_hist(const uint32_t* __restrict__ cost, int n, int gx, int r,
-                                                      uint32_t* __restrict__ hist) {
+                                                      uint32_t* __restrict__ hist, uint8_t* __restrict__ bucket) {
     __shared__ uint32_t h[kSchedBuckets];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const int end = min(n, (int)(blockIdx.x + 1) * 1024);
-    for (int i = blockIdx.x * 1024 + threadIdx.x; i < end; i += 256) atomicAdd(&h[sched_bucket(tile_key(cost, i, n, gx, r))], 1u);
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const int b = sched_bucket(r == 2 ? tile_key_r<2>(cost, i, n, gx) : tile_key(cost, i, n, gx, r));
+        bucket[i] = (uint8_t)b;
+        atomicAdd(&h[b], 1u);
+    }
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restrict__ cost, int n, int gx, int r,
+__global__ __launch_bounds__(256) void rm_sched_scatter(const uint8_t* __restrict__ bucket, int n,
                                                          const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor,
                                                          uint32_t* __restrict__ order, uint32_t* __restrict__ next) {
     __shared__ uint32_t base[kSchedBuckets], cnt[kSchedBuckets];
@@ -186,7 +210,7 @@ __global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restri
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int i = i0 + 256 * k;
-        b[k] = i < n ? sched_bucket(tile_key(cost, i, n, gx, r)) : -1;
+        b[k] = i < n ? (int)bucket[i] : -1;
         rank[k] = b[k] >= 0 ? atomicAdd(&cnt[b[k]], 1u) : 0;
     }
     __syncthreads();
@@ -198,11 +222,11 @@ __global__ __launch_bounds__(256) void rm_sched_scatter(const uint32_t* __restri
 }
 
 hipError_t launch_tile_order(const uint32_t* cost, int n, int gx, int radius, uint32_t* order, uint32_t* hist,
-                             uint32_t* next, hipStream_t s) {
+                             uint32_t* next, uint8_t* bucket, hipStream_t s) {
     if (n <= 0 || gx <= 0) return hipSuccess;
-    const unsigned blocks = (unsigned)((n + 1023) / 1024);
-    hipLaunchKernelGGL(rm_sched_hist, dim3(blocks), dim3(256), 0, s, cost, n, gx, radius, hist);
-    hipLaunchKernelGGL(rm_sched_scatter, dim3(blocks), dim3(256), 0, s, cost, n, gx, radius, hist,
+    hipLaunchKernelGGL(rm_sched_hist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cost, n, gx, radius, hist,
+                       bucket);
+    hipLaunchKernelGGL(rm_sched_scatter, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, s, bucket, n, hist,
                        hist + kSchedBuckets, order, next);
     return hipGetLastError();
 }

@@ -47,7 +47,7 @@ hipError_t launch_deinterleave_cycle_rgb8(const uint8_t* gathered, uint32_t* out
 // (hist: 256 counts + 256 cursors, zero on entry); clears `next` (512 words)
 // for the following launch
 hipError_t launch_tile_order(const uint32_t* cost, int n, int gx, int radius, uint32_t* order, uint32_t* hist,
-                             uint32_t* next, hipStream_t s);
+                             uint32_t* next, uint8_t* bucket, hipStream_t s);
 hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 // rm_wire.hip: the compressed RGB wire of RGBA8 row parts
 long long wire_capacity(int W, int n);
