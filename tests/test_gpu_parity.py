@@ -1044,3 +1044,34 @@ def test_compressed_wire_pipelined_in_one_process(R, torch_cuda, runs):
     for g, ref in zip(got, refs):
         assert np.array_equal(g, ref)
     r1.close()
+
+
+def test_context_outlives_a_destroyed_stream(torch_cuda):
+    """Completion events are recorded lazily: when the
+    context leaves a stream, the event goes on that stream while it still
+    exists.  Render on a raw HIP stream, switch away, destroy the stream, keep
+    rendering (adaptive order across streams), then destroy the context: no
+    wait on a dead stream, and the frames stay right."""
+    import ctypes
+    torch = torch_cuda
+    hip = ctypes.CDLL("libamdhip64.so")
+    r = rm.Renderer(0)
+    setup(r, "T", POSES["P2"], 64)
+    r.set_params(count_evals=0, schedule=1)
+    ref = r.render_rgba8(64, 48)
+    torch.cuda.synchronize()
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(st), ctypes.c_uint(1)) == 0
+    out = torch.empty((48, 64), dtype=torch.int32, device="cuda")
+    r.set_stream(st.value)
+    for _ in range(10):  # an adaptive order is built on the raw stream
+        r.render_rgba8(64, 48, out=out)
+    r.set_stream(torch.cuda.current_stream())
+    assert hip.hipStreamSynchronize(st) == 0
+    assert torch.equal(out, ref)
+    assert hip.hipStreamDestroy(st) == 0
+    for _ in range(3):
+        out2 = r.render_rgba8(64, 48)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, ref)
+    r.close()
