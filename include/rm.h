@@ -63,7 +63,7 @@ typedef struct rm_params {
                                  4 8x8 px tiles pulled by persistent waves from an atomic counter (built-in scenes) */
     int32_t schedule;         /* dispatch order of one-wave tiles: 1 (default) = the costliest tiles of a recent
                                  launch of the same geometry on the same stream first (their measured durations,
-                                 counting-sorted on the GPU right after every 8th launch, on its stream,
+                                 counting-sorted on the GPU right after every 16th launch, on its stream,
                                  RM_SCHED_PERIOD; the first launch of a geometry runs row-major); 0 = row-major.
                                  Pixels are the same either way; an rm_set_tile_order order takes precedence. */
 } rm_params;

@@ -333,11 +333,14 @@ int lat_tiles() {
 // frame 0.683 -> 0.672 ms against 1); after the round-3 skips the frame is
 // shorter and 8 measured 0.7 % (still) and 1.8 % (walking) faster than 4, 16
 // the same as 8 (profiles/r03/sched_period_after_skips.jsonl).
+// Round 4 sorts on the frame's stream (21 us per sort in the frame's time):
+// 16 measured 0.3-0.7 % faster than 8 still, walking and at P1, 4 slower
+// (profiles/r04/sched_knobs_final_ab.log, sched_period_walk_p1_ab.log).
 // RM_SCHED_PERIOD overrides it (1 = re-sort after every launch).
 int sched_period() {
     static const int n = [] {
         const char *e = std::getenv("RM_SCHED_PERIOD");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 8;
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 16;
     }();
     return n;
 }
