@@ -83,6 +83,8 @@ def parse():
                     help="tile dispatch order: costliest tiles of the previous frame first, or row-major")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
+    ap.add_argument("--dist-timeout", type=float, default=180.0,
+                    help="N > 1: seconds any one collective may take before the run fails (init_process_group timeout)")
     ap.add_argument("--walk", action="store_true",
                     help="moving camera and advancing u_time (main.cpp's W key at 60 Hz) instead of a still pose")
     ap.add_argument("--walk-speed", type=float, default=0.1, help="camera step per frame (main.cpp:21 speed)")
@@ -285,43 +287,80 @@ def balanced_runs(world, band, H, ex):
     return [r0] + [band] * (world - 1), dict(T1_ms=T1, G_ms=G, deinterleave_ms=d, share_other=s, share_root=s0)
 
 
-def roofline(pmc, flop_tally, evals, ref_flop_per_step, kern_ms, out_bytes):
-    """The render kernel's FP32-VALU roofline.  With PMC counters of this
-    workload (profiles/pmc_counters.json, rocprofv3 --pmc of the same command):
-    executed FP32 FLOP = (ADD + MUL + TRANS + 2 FMA) F32 wave-instructions x 64
-    lanes per launch, over this run's live kernel time.  Without: the
-    instrumented per-term tally (SURVEY.md 8(d) prices over the terms
-    evaluated).  VALU/SALU issue fractions beside it."""
+_F32_KEYS = ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32")
+
+
+def pmc_flop(pmc):
+    """(FP32 FLOP done by active lanes in one PMC-counted launch, issued lane
+    slots, active-lane fraction), or None without the F32 counters:
+    64 x (ADD + MUL + TRANS + 2 FMA) wave-instructions, scaled by the mean
+    active-lane fraction SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)."""
+    if not all(k in pmc for k in _F32_KEYS):
+        return None
+    slots = 64 * (pmc[_F32_KEYS[0]] + pmc[_F32_KEYS[1]] + pmc[_F32_KEYS[2]] + 2 * pmc[_F32_KEYS[3]])
+    lane_frac = pmc.get("active_lane_frac")
+    return slots * (lane_frac or 1.0), slots, lane_frac
+
+
+def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=True, rows_frac=1.0):
+    """The render kernel's FP32-VALU roofline for one launch of kern_ms that
+    executed `executed_steps` ray-steps and wrote out_bytes.
+
+    pmc holds rocprofv3 --pmc counters (profiles/pmc_counters.json) of one N = 1
+    launch.  exact: they are counters of this very workload (same frame, pose,
+    build): FLOP = the counted FLOP.  Otherwise (a rank's share of that frame
+    for N > 1, or a walk): FLOP = executed_steps x (the counted FLOP / the
+    counted launch's executed ray-steps), and the HBM traffic = the counted
+    traffic x rows_frac.  With no counters the FP32 FLOP are not known and frac
+    is null with the reason: the instrumented per-term tally (SURVEY.md 8(d)
+    prices over the terms evaluated, incl. work exact exits skip) is reported as
+    tally_frac only, never as frac."""
+    if not kern_ms or kern_ms <= 0:  # a rank with no rows launches nothing
+        return {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
+                "traffic": None, "frac_null_reason": "no launch (no rows on this rank)"}
     t = kern_ms / 1e3
-    keys = ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32")
-    slots, lane_frac = None, None
-    if all(k in pmc for k in keys):
-        # issued FP32 lane slots (64 per wave-instruction), scaled by the mean
-        # active-lane fraction of VALU instructions (exec mask): the FLOP that
-        # active lanes did
-        slots = 64 * (pmc[keys[0]] + pmc[keys[1]] + pmc[keys[2]] + 2 * pmc[keys[3]])
-        lane_frac = pmc.get("active_lane_frac")
-        flop = slots * (lane_frac or 1.0)
-        src = (f"PMC executed FP32 ops ({pmc.get('source')}): 64 x (ADD + MUL + TRANS + 2 FMA)"
-               + (" x active-lane fraction SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)" if lane_frac else
-                  " (issued lane slots: no active-lane counter for this workload)"))
+    cnt = pmc_flop(pmc) if pmc else None
+    base_steps = pmc.get("executed_ray_steps_per_launch") if pmc else None
+    roof = {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
+            "traffic": None, "flop_per_launch": None, "executed_ray_steps_per_launch": executed_steps,
+            "ray_steps_per_launch": evals, "kernel_ms": kern_ms}
+    if cnt is not None and (exact or base_steps):
+        flop_c, slots, lane_frac = cnt
+        if exact:
+            flop = flop_c
+            src = (f"PMC executed FP32 ops of this workload ({pmc.get('source')}): 64 x (ADD + MUL + TRANS + 2 FMA)"
+                   + (" x active-lane fraction" if lane_frac else " (issued lane slots)"))
+        else:
+            per_step = flop_c / base_steps
+            flop = executed_steps * per_step
+            slots = slots * executed_steps / base_steps
+            src = (f"this launch's executed ray-steps x the PMC FP32 FLOP per executed ray-step of the N = 1 launch "
+                   f"of the same workload ({pmc.get('source')}: {flop_c:.4g} FLOP / {base_steps} steps = "
+                   f"{per_step:.2f})")
+        ach = flop / t / 1e12
+        roof.update(achieved=ach, frac=ach / PEAK_FP32_TFLOPS, flop_per_launch=flop, flop_source=src,
+                    active_lane_frac=lane_frac, issued_lane_slot_frac=slots / t / 1e12 / PEAK_FP32_TFLOPS)
+        if pmc.get("hbm_bytes_per_launch") is not None:
+            roof["traffic"] = pmc["hbm_bytes_per_launch"] * (1.0 if exact else rows_frac)
     else:
-        flop = flop_tally
-        src = "instrumented tally (no PMC counters for this workload in profiles/)"
-    ach = flop / t / 1e12
-    roof = {
-        "bound": "valu", "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-        "frac": ach / PEAK_FP32_TFLOPS, "traffic": pmc.get("hbm_bytes_per_launch"),
-        "flop_per_launch": flop, "flop_source": src, "ray_steps_per_launch": evals,
-        "issued_lane_slot_flop_per_launch": slots, "active_lane_frac": lane_frac,
-        "issued_lane_slot_frac": None if slots is None else slots / t / 1e12 / PEAK_FP32_TFLOPS,
-        "tally_flop_per_launch": flop_tally, "tally_tflops": flop_tally / t / 1e12,
-        "reference_tally_flop_per_ray_step": ref_flop_per_step,
-        "reference_equivalent_tflops": evals * ref_flop_per_step / t / 1e12,
-        "hbm": {"achieved": out_bytes / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": out_bytes / t / 1e9 / PEAK_HBM_GBS, "algorithmic_bytes_per_launch": out_bytes},
-    }
-    if "SQ_INSTS_VALU" in pmc:
+        roof["frac_null_reason"] = (
+            "no PMC counters for this workload in profiles/pmc_counters.json" if cnt is None else
+            "the PMC entry of this workload has no executed_ray_steps_per_launch to price a share of it")
+    roof["tally_flop_per_launch"] = flop_tally
+    roof["tally_frac"] = None if flop_tally is None else flop_tally / t / 1e12 / PEAK_FP32_TFLOPS
+    roof["tally_note"] = ("SURVEY 8(d) per-term price list over the reference terms the instrumented kernel "
+                          "evaluates; not executed FP32 FLOP (abs/min/max are free modifiers or med3), not the "
+                          "roofline figure")
+    gbs = out_bytes / t / 1e9
+    roof["hbm"] = {"achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                   "algorithmic_bytes_per_launch": out_bytes, "counter_gbs": None, "counter_frac": None}
+    if roof["traffic"] is not None:
+        cg = roof["traffic"] / t / 1e9
+        roof["hbm"].update(counter_gbs=cg, counter_frac=cg / PEAK_HBM_GBS,
+                           counter_note="rocprofv3 (2 FETCH_SIZE + WRITE_SIZE) per launch"
+                                        + ("" if exact else " of the N = 1 frame x this launch's row fraction")
+                                        + " / kernel_ms")
+    if exact and pmc and "SQ_INSTS_VALU" in pmc:
         # issue fractions at the clock the PMC run measured (GRBM_GUI_ACTIVE / 8 XCDs / kernel time):
         # one wave64 VALU instruction per 2 cycles per SIMD (1024 SIMDs), one SALU per cycle per CU (256)
         clk = pmc.get("clock_hz") or 2.4e9
@@ -351,10 +390,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
+        # a finite timeout on every collective: a first real RCCL exchange that
+        # stalls ends the run non-zero with the watchdog's message (the default
+        # would wait 10 min per collective) instead of hanging the driver
+        import datetime
+        to = datetime.timedelta(seconds=args.dist_timeout)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")  # tear down on timeout
+            dist.init_process_group("nccl", device_id=dev, timeout=to)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=to)
 
     W = args.size
     H = args.height or args.size
@@ -473,6 +518,8 @@ def main():
         dist.all_reduce(ev_total)
     evals_rank, evals_frame = int(ev_rank[0].item()), int(ev_total[0].item())
     skipped_frame = int(ev_total[1].item())
+    exec_rank = evals_rank - int(ev_rank[1].item())  # ray-steps this rank's launch executes
+    rank_launch = [dict(kernel_ms=None, executed_steps=exec_rank, rows=fr.nmine)]
 
     # untimed spin-up before the W warm-up frames: a fresh GPU ramps its clocks
     # over the first ~0.1 s of load (3 warm-up frames are ~3 ms), so the timed
@@ -539,16 +586,17 @@ def main():
             wire_sizes = [int(v) for v in xs[-1]["wire_bytes"]]
         else:
             wire_sizes = [fr.plan.count(q) * wire_row for q in range(world)]
-        mine = torch.tensor([kern] + [_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
-                                                                                "deinterleave_ms")],
-                            dtype=torch.float64, device=red_dev)
+        mine = torch.tensor([kern, exec_rank, fr.nmine] + [_median([x[k] for x in xs]) for k in (
+            "render_ms", "pack_ms", "gather_ms", "deinterleave_ms")], dtype=torch.float64, device=red_dev)
         per_rank = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(per_rank, mine)
         pr = [[float(v) for v in x.cpu()] for x in per_rank]
+        rank_launch = [dict(kernel_ms=x[0], executed_steps=int(x[1]), rows=int(x[2])) for x in pr]
         exchange = {
-            "gather_ms": pr[0][3], "deinterleave_ms": pr[0][4], "pack_ms": pr[0][2],
-            "kernel_ms_per_rank": [x[0] for x in pr], "gather_ms_per_rank": [x[3] for x in pr],
-            "pack_ms_per_rank": [x[2] for x in pr],
+            "gather_ms": pr[0][5], "deinterleave_ms": pr[0][6], "pack_ms": pr[0][4],
+            "kernel_ms_per_rank": [x[0] for x in pr], "gather_ms_per_rank": [x[5] for x in pr],
+            "pack_ms_per_rank": [x[4] for x in pr],
+            "executed_ray_steps_per_rank": [int(x[1]) for x in pr], "rows_per_rank": [int(x[2]) for x in pr],
             "wire_bytes_per_rank": wire_sizes,
             "root_ingress_bytes": sum(wire_sizes[1:]),
             "wire": fr.wire,
@@ -565,19 +613,28 @@ def main():
     elapsed, kern_max = float(t.item()), float(kt.item())
 
     if rank == 0:
-        F = rm.FLOP_PER_EVAL[args.scene]
         flop_rank = st["flop"]
-        out_bytes = W * fr.plan.count(0) * (4 if args.fmt == "rgba8" else 16)  # the frame the kernel writes
         pmc = {}
         try:
             pm = json.load(open(args.pmc))
-            # (a walk renders other poses than the still frame the counters were taken on)
-            key = (f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}" + ("" if world == 1 else f"_n{world}")
-                   + ("_walk" if args.walk else ""))
-            pmc = pm.get(key, {})
+            # counters of one N = 1 launch of this frame at this pose (a rank's
+            # share, or a walk's other poses, are priced per executed ray-step)
+            pmc = pm.get(f"{args.scene}_{W}x{H}_{args.max_steps}_{args.pose}", {})
         except (OSError, ValueError):
             pass
-        roof = roofline(pmc, flop_rank, evals_rank, F, kern, out_bytes)
+        exact = world == 1 and not args.walk
+        rank_launch[0]["kernel_ms"] = kern
+        # the roofline's launch: the slowest rank's (kernel_ms_max_rank), priced
+        # by its own executed ray-steps; every rank's beside it
+        crit = max(range(len(rank_launch)), key=lambda q: rank_launch[q]["kernel_ms"])
+        cl = rank_launch[crit]
+        roof = roofline(pmc, cl["kernel_ms"], cl["executed_steps"],
+                        W * cl["rows"] * (4 if args.fmt == "rgba8" else 16), flop_rank if crit == 0 else None,
+                        evals_rank if crit == 0 else None, exact=exact, rows_frac=cl["rows"] / H)
+        if world > 1:
+            roof["rank"] = crit
+            roof["per_rank_frac"] = [roofline(pmc, q["kernel_ms"], q["executed_steps"], 0, None, None, exact=False,
+                                              rows_frac=q["rows"] / H)["frac"] for q in rank_launch]
         res = {
             "metric": "ray-steps/sec + frames/sec at 4096\u00d74096, 1/2/4/8 MI355X",
             "value": evals_frame * args.steps / elapsed,

@@ -103,6 +103,9 @@ int rm_abi_version(void);
 
 /* Create a context on HIP device `device`.  Scene unset, params default. */
 rm_status rm_create(rm_ctx **out, int device);
+/* Waits for the work this context enqueued (its own events, not the device),
+ * then frees it.  If the stream it is bound to was destroyed meanwhile (see
+ * rm_set_stream), it falls back to waiting for the whole device. */
 rm_status rm_destroy(rm_ctx *ctx);
 
 /* Replaces ShaderLoader::loadFromFile (source/shader_loader.cpp:8-20).
@@ -156,7 +159,11 @@ rm_status rm_set_uniform3f(rm_ctx *ctx, const char *name, float x, float y, floa
 rm_status rm_set_params(rm_ctx *ctx, const rm_params *params);
 rm_status rm_get_params(rm_ctx *ctx, rm_params *params);
 
-/* Stream the ctx launches on (a hipStream_t; NULL = the null stream). */
+/* Stream the ctx launches on (a hipStream_t; NULL = the null stream).
+ * Lifetime: a stream must outlive its binding.  Before destroying a stream the
+ * context is bound to, bind another one (e.g. rm_set_stream(ctx, NULL)): that
+ * records the context's completion events on the old stream while it exists.
+ * Streams the context has left may be destroyed at any time. */
 rm_status rm_set_stream(rm_ctx *ctx, void *hip_stream);
 rm_status rm_synchronize(rm_ctx *ctx);
 

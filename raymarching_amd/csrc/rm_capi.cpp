@@ -136,20 +136,26 @@ hipError_t record_sched_last(rm_ctx *ctx) {
 }
 
 // The KERNEL_PERSIST counter block of the ctx stream (rm_ctx::PersistBlock).
+// A new block joins ctx->persist only once its event and counters exist (a
+// half-built block would match the null stream with a null counter array).
 rm_status persist_block(rm_ctx *ctx, rm_ctx::PersistBlock *&out) {
-    static uint64_t clock = 0;
     out = nullptr;
     for (auto &b : ctx->persist)
         if (b.stream == ctx->stream) out = &b;
     if (!out && (int)ctx->persist.size() < rm_ctx::kPersistBlocks) {
-        ctx->persist.emplace_back();
-        rm_ctx::PersistBlock &b = ctx->persist.back();
+        rm_ctx::PersistBlock b{};
         const size_t bytes = (size_t)rm::kPersistWords * sizeof(uint32_t);
         RM_HIP(hipEventCreateWithFlags(&b.last, hipEventDisableTiming));
-        RM_HIP(hipMalloc(&b.ctr, bytes));
-        RM_HIP(hipMemsetAsync(b.ctr, 0, bytes, ctx->stream));
+        hipError_t e = hipMalloc(&b.ctr, bytes);
+        if (e == hipSuccess) e = hipMemsetAsync(b.ctr, 0, bytes, ctx->stream);
+        if (e != hipSuccess) {
+            if (b.ctr) (void)hipFree(b.ctr);
+            (void)hipEventDestroy(b.last);
+            return hip_fail(ctx, e, "persist_block: counter block");
+        }
         b.stream = ctx->stream;
-        out = &b;
+        ctx->persist.push_back(b);
+        out = &ctx->persist.back();
     }
     if (!out) {  // recycle the least recently used block once its last launch is done
         out = &ctx->persist[0];
@@ -158,7 +164,7 @@ rm_status persist_block(rm_ctx *ctx, rm_ctx::PersistBlock *&out) {
         RM_HIP(hipEventSynchronize(out->last));
         out->stream = ctx->stream;
     }
-    out->used = ++clock;
+    out->used = ++ctx->sched_clock;  // per-context LRU clock (shared with the sched entries)
     return RM_OK;
 }
 
@@ -326,10 +332,10 @@ int lat_tiles() {
     return n;
 }
 
-// Launches per dispatch-order sort of a geometry (rm_ctx::Sched): 8 -- an
-// order is at most 9 launches old (frame-to-frame coherence keeps it good, the
+// Launches per dispatch-order sort of a geometry (rm_ctx::Sched): 16 -- an
+// order is at most 17 launches old (frame-to-frame coherence keeps it good, the
 // dilated key covers a moving camera), and the duration stores, the sort and
-// the cross-stream events run on one launch in eight.  Round 2 chose 4 (C3
+// the cross-stream events run on one launch in sixteen.  Round 2 chose 4 (C3
 // frame 0.683 -> 0.672 ms against 1); after the round-3 skips the frame is
 // shorter and 8 measured 0.7 % (still) and 1.8 % (walking) faster than 4, 16
 // the same as 8 (profiles/r03/sched_period_after_skips.jsonl).
@@ -723,9 +729,18 @@ rm_status rm_destroy(rm_ctx *ctx) {
     // nothing this context enqueued still runs: its own events (the streams
     // it left may be the caller's and gone by now); other work on the device
     // is not waited for
-    (void)record_sched_last(ctx);
-    if (ctx->done && ctx->dirty && hipEventRecord(ctx->done, ctx->stream) == hipSuccess)
-        (void)hipEventSynchronize(ctx->done);
+    // A record that fails means the bound stream is gone (destroyed while the
+    // context was still bound to it, against rm.h's rule): the context's work
+    // on it can no longer be waited for by event, so the whole device is.
+    bool lost = record_sched_last(ctx) != hipSuccess;
+    if (ctx->done && ctx->dirty) {
+        if (hipEventRecord(ctx->done, ctx->stream) == hipSuccess) (void)hipEventSynchronize(ctx->done);
+        else lost = true;
+    }
+    if (lost) {
+        (void)hipGetLastError();
+        (void)hipDeviceSynchronize();
+    }
     for (hipEvent_t ev : ctx->retired) {
         (void)hipEventSynchronize(ev);
         (void)hipEventDestroy(ev);

@@ -343,22 +343,24 @@ __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& 
 #endif
 }
 
-// (the probe form's sum of squares fused: RM_PROBE_FMA_O, rm_render_direct.h)
+// FUSE_O: scene O's probe form (its sphere and cube distances, !EXACT) fuses
+// the sum of squares (RM_PROBE_FMA_O, rm_render_direct.h); every other caller
+// (scene S0's sphere) keeps the unfused form
 #ifndef RM_PROBE_FMA_O
 #define RM_PROBE_FMA_O 1
 #endif
-template <bool EXACT>
+template <bool EXACT, bool FUSE_O = false>
 __device__ __forceinline__ float len3(float x, float y, float z) {
-    if constexpr (!EXACT && RM_PROBE_FMA_O) return __builtin_amdgcn_sqrtf(fmaf(z, z, fmaf(y, y, x * x)));
+    if constexpr (!EXACT && FUSE_O && RM_PROBE_FMA_O) return __builtin_amdgcn_sqrtf(fmaf(z, z, fmaf(y, y, x * x)));
     float l2 = x * x + y * y + z * z;
     return EXACT ? sqrtf(l2) : __builtin_amdgcn_sqrtf(l2);
 }
 
-// cube(vec4(c, r), p) (common.frag:589-593)
+// cube(vec4(c, r), p) (common.frag:589-593), scene O's
 template <bool EXACT>
 __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
     float qx = fabsf(p.x - c.x) - r, qy = fabsf(p.y - c.y) - r, qz = fabsf(p.z - c.z) - r;
-    return len3<EXACT>(fmaxf(qx, 0.0f), fmaxf(qy, 0.0f), fmaxf(qz, 0.0f)) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f);
+    return len3<EXACT, true>(fmaxf(qx, 0.0f), fmaxf(qy, 0.0f), fmaxf(qz, 0.0f)) + fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f);
 }
 
 // scene O's sceneSDF distance (output_shader.frag:38-48) at world point p with
@@ -419,7 +421,7 @@ __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n, float& slack
         if (d0 + 0.34f <= A) return d0;
     }
     n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
-    const float d1 = len3<EXACT>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
+    const float d1 = len3<EXACT, true>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
     const float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
     const float t1 = smin_cubic_d<EXACT>(d1, d2, 0.5f, m);
     const float t2 = smin_cubic_d<EXACT>(t1, d3, 0.5f, m);

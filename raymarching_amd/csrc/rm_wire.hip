@@ -155,13 +155,13 @@ __global__ __launch_bounds__(64) void rm_wire_decode(const uint8_t* __restrict__
     const size_t hb = wire_header_bytes(n, S);
     const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
     const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
-    const int cnt = counts[k];
+    const int cnt = min((int)counts[k], kSegWords);  // (a corrupt count cannot read past the segment)
     const uint64_t* sw = reinterpret_cast<const uint64_t*>(msg + hb) + off;
     const uint64_t mine = l < cnt ? sw[l] : 0ull;  // lane 0: header, lane q + 1: plane q
     const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
     const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_lo);
     const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_hi);
-    const int b[3] = {(int)((h_lo >> 24) & 15u), (int)(h_lo >> 28), (int)(h_hi & 15u)};
+    const int b[3] = {min((int)((h_lo >> 24) & 15u), 8), min((int)(h_lo >> 28), 8), min((int)(h_hi & 15u), 8)};
     // this lane's bit of a plane word: from the low half for lanes 0-31, the high half for 32-63
     const uint32_t sh = (uint32_t)(l & 31);
     const bool hi_half = l >= 32;
@@ -197,13 +197,13 @@ __global__ __launch_bounds__(64) void rm_wire_decode_parts(WireParts parts, int 
         const uint8_t* msg = P.msg;
         const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
         const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
-        const int cnt = counts[k];
+        const int cnt = min((int)counts[k], kSegWords);
         const uint64_t* sw = reinterpret_cast<const uint64_t*>(msg + hb) + off;
         const uint64_t mine = l < cnt ? sw[l] : 0ull;
         const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
         const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_lo);
         const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_hi);
-        const int b[3] = {(int)((h_lo >> 24) & 15u), (int)(h_lo >> 28), (int)(h_hi & 15u)};
+        const int b[3] = {min((int)((h_lo >> 24) & 15u), 8), min((int)(h_lo >> 28), 8), min((int)(h_hi & 15u), 8)};
         const uint32_t sh = (uint32_t)(l & 31);
         const bool hi_half = l >= 32;
         uint32_t px = 0;

@@ -653,6 +653,7 @@ class DeltaFrame(DistributedFrame):
                 dist.all_gather_into_tensor(allsz, sz, group=self.group)
                 sizes = [int(v) for v in allsz.cpu()]
                 if self.rank == 0:
+                    self._check_sizes(slot, sizes)
                     if self.decoded_recorded[slot]:
                         self.ctrl.wait_event(self.decoded[slot])  # the slot's last decode has read its buffers
                     ops = [dist.P2POp(dist.irecv, self.recv[slot][q][: sizes[q]], q, group=self.group)
@@ -664,6 +665,7 @@ class DeltaFrame(DistributedFrame):
         dist.all_gather(allsz, torch.tensor([mine], dtype=torch.int64), group=self.group)
         sizes = [int(v[0]) for v in allsz]
         if self.rank == 0:
+            self._check_sizes(slot, sizes)
             for q in range(1, self.world):
                 buf = torch.empty(sizes[q], dtype=torch.uint8)
                 dist.recv(buf, src=q, group=self.group)
@@ -671,6 +673,17 @@ class DeltaFrame(DistributedFrame):
         else:
             dist.send(self.msg[slot][:mine].cpu(), dst=0, group=self.group)
         return sizes, []
+
+    def _check_sizes(self, slot, sizes):
+        """The peers' message sizes against the receive buffers (wire
+        capacity): a larger one would be truncated and the send/receive
+        lengths would no longer match (a hang or a corrupt decode), so it
+        fails here instead."""
+        for q in range(1, self.world):
+            cap = self.recv[slot][q].numel()
+            if not 0 <= sizes[q] <= cap:
+                raise RuntimeError(f"DeltaFrame: rank {q} reports a {sizes[q]}-byte message; the receive buffer "
+                                   f"holds {cap} (wire capacity)")
 
     def _decode(self, slot, st):
         p = self.plan

@@ -40,6 +40,19 @@ POLICY = {
 }
 
 
+# Full-size frames (C2/C3/C5, tests/test_gpu_parity.py full_size_parity): the
+# levels the HIP path achieves there (round 4: C3 f2e3 0.999997, C2 >= 0.99998,
+# C5 1.0), ratcheted so that a regression moving 0.01 % of a frame (1.7 k
+# pixels at 4096^2) fails; the small golden frames keep POLICY above.
+FULL_SIZE_POLICY = {
+    "T": dict(f2e3=0.9999, f1e2=0.99995, mean=1e-4),
+    "O": dict(f2e3=0.9999, f1e2=0.99995, mean=1e-4),
+}
+# per-pixel ray-step maps at full size: fraction of pixels whose sceneSDF call
+# count equals the oracle's (achieved: T 0.9985-0.9999, O 1.00000)
+FULL_SIZE_STEP_MAP = {"T": 0.998, "O": 0.9999}
+
+
 def assert_parity(scene, a, b, policy=None, label=""):
     p = dict(POLICY[scene] if policy is None else policy)
     s = diff_stats(a, b)

@@ -30,6 +30,26 @@ def _run(cmd):
     return json.loads(lines[0])
 
 
+def _rates_within_peak(d):
+    """Every achieved rate of the line is at most its peak, and frac is never
+    the instrumented tally's (PMC-priced, or null with a reason)."""
+    if isinstance(d, dict):
+        if d.get("achieved") is not None and d.get("peak"):
+            assert d["achieved"] <= d["peak"], d
+        for v in d.values():
+            _rates_within_peak(v)
+
+
+def _check_roofline(res):
+    roof = res["roofline"]
+    _rates_within_peak(res)
+    assert "reference_equivalent_tflops" not in roof and "tally_tflops" not in roof, roof
+    if roof["frac"] is None:
+        assert roof["frac_null_reason"], roof
+    else:
+        assert "PMC" in roof["flop_source"] and roof["frac"] < 1, roof
+
+
 def _torchrun(n, extra):
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
             "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(n)] + extra
@@ -41,6 +61,8 @@ def test_bench_one_gpu_frame_check(torch_cuda, scene):
     res = _run([sys.executable, "bench.py"] + SMALL + ["--scene", scene])
     assert res["frame_check"]["result"] == "bit-exact" and res["frame_check"]["pixels"] == 512 * 512, res
     assert res["n_gpus"] == 1 and "gather_ms" not in res
+    _check_roofline(res)
+    assert res["roofline"]["frac"] is None  # no counters for a 512x512 frame
 
 
 @pytest.mark.gpu
@@ -53,6 +75,9 @@ def test_bench_two_ranks_gloo_rehearsal(torch_cuda):
     assert res["gather_ms"] > 0 and res["deinterleave_ms"] > 0 and res["backend"] == "gloo", res
     assert res["root_ingress_bytes"] == 256 * 3 * 512 and res["wire_bytes_per_rank"] == [256 * 3 * 512] * 2, res
     assert res["balance"] == {"mode": "even", "chosen": "even/rgb8", "runs": [16, 16], "wire": "rgb8"}, res
+    _check_roofline(res)
+    assert len(res["roofline"]["per_rank_frac"]) == 2 and res["roofline"]["rank"] in (0, 1), res
+    assert sum(res["executed_ray_steps_per_rank"]) == res["config"]["executed_ray_steps_per_frame"], res
 
 
 @pytest.mark.gpu

@@ -1,0 +1,90 @@
+"""bench.py's roofline(): frac comes from PMC-counted FP32 FLOP only -- for the
+counted launch itself, or per executed ray-step for a share of it (N > 1) --
+never from the instrumented tally, and no rate in it exceeds its peak (host
+logic, no GPU)."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+PMC = json.load(open(os.path.join(ROOT, "profiles", "pmc_counters.json")))
+C3 = PMC["T_4096x4096_256_P0"]
+
+
+def _rates(d, path=""):
+    """(path, value, peak) of every achieved/peak pair in the line."""
+    out = []
+    if isinstance(d, dict):
+        if d.get("achieved") is not None and d.get("peak"):
+            out.append((path, d["achieved"], d["peak"]))
+        for k, v in d.items():
+            out += _rates(v, f"{path}.{k}")
+    return out
+
+
+def test_exact_launch_uses_counted_flop():
+    ms = C3["avg_kernel_ns_trace"] / 1e6
+    r = bench.roofline(C3, ms, C3["executed_ray_steps_per_launch"], 4096 * 4096 * 4, 9e13, 1e9)
+    flop = bench.pmc_flop(C3)[0]
+    assert r["flop_per_launch"] == pytest.approx(flop)
+    assert r["frac"] == pytest.approx(flop / (ms / 1e3) / 1e12 / bench.PEAK_FP32_TFLOPS)
+    assert 0.2 < r["frac"] < 0.5
+    # the tally (here a nonsense 9e13) stays out of frac
+    assert r["tally_frac"] > 1 and r["frac"] < 1
+    assert r["hbm"]["counter_gbs"] == pytest.approx(C3["hbm_bytes_per_launch"] / (ms / 1e3) / 1e9)
+    assert "reference_equivalent_tflops" not in r and "tally_tflops" not in r
+    assert all(v <= p for _, v, p in _rates(r))
+
+
+@pytest.mark.parametrize("share", [0.5, 0.8, 0.125])
+def test_rank_share_priced_per_executed_step(share):
+    """A rank that executes a share of the frame's steps in the same time per
+    step as the whole frame gets the N = 1 fraction, whatever its share."""
+    ms = C3["avg_kernel_ns_trace"] / 1e6
+    base = bench.roofline(C3, ms, C3["executed_ray_steps_per_launch"], 1, None, None)
+    steps = int(C3["executed_ray_steps_per_launch"] * share)
+    r = bench.roofline(C3, ms * share, steps, 1, 5e10, 1e9, exact=False, rows_frac=share)
+    assert r["frac"] == pytest.approx(base["frac"], rel=1e-6)
+    assert r["traffic"] == pytest.approx(C3["hbm_bytes_per_launch"] * share)
+    assert "per executed ray-step" in r["flop_source"]
+    assert "valu_issue" not in r  # issue fractions are counters of the counted launch only
+
+
+def test_tally_never_becomes_frac():
+    """No counters (or counters without the executed-steps anchor for a share):
+    frac is null with a reason, whatever the tally says."""
+    r = bench.roofline({}, 0.45, 5e8, 1, 5.3e10, 1e9)
+    assert r["frac"] is None and r["achieved"] is None and "no PMC" in r["frac_null_reason"]
+    assert r["tally_frac"] == pytest.approx(5.3e10 / 0.45e-3 / 1e12 / bench.PEAK_FP32_TFLOPS)
+    no_anchor = {k: v for k, v in C3.items() if k != "executed_ray_steps_per_launch"}
+    r = bench.roofline(no_anchor, 0.2, 2.6e8, 1, 5.3e10, 1e9, exact=False, rows_frac=0.5)
+    assert r["frac"] is None and "executed_ray_steps" in r["frac_null_reason"]
+
+
+def test_no_rows_no_launch():
+    r = bench.roofline(C3, 0.0, 0, 0, None, None, exact=False)
+    assert r["frac"] is None
+
+
+def test_r04_n2_rehearsal_reprices_within_5pct():
+    """Round 4's gloo N = 2 rehearsal line (balanced runs [1089, 16]: rank 0
+    rendered 98.6 % of the rows in 0.4535 ms) printed frac 0.742 from the
+    tally.  Priced per executed ray-step its launch lands within 5 % of the
+    N = 1 counted fraction, as the same kernel over nearly the same rows must."""
+    ms = C3["avg_kernel_ns_trace"] / 1e6
+    base = bench.roofline(C3, ms, C3["executed_ray_steps_per_launch"], 1, None, None)["frac"]
+    n2 = json.load(open(os.path.join(ROOT, "profiles", "r04", "bench_n2_gloo_r04final2.json")))
+    runs = n2["balance"]["runs"]
+    share = runs[0] / sum(runs)
+    steps = int(C3["executed_ray_steps_per_launch"] * share)
+    r = bench.roofline(C3, n2["kernel_ms_per_rank"][0], steps, 1, n2["roofline"]["tally_flop_per_launch"], None,
+                       exact=False, rows_frac=share)
+    assert n2["roofline"]["frac"] > 0.7  # the old, tally-based figure
+    assert r["frac"] == pytest.approx(base, rel=0.05)
+    assert r["tally_frac"] > 0.7

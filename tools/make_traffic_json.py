@@ -14,7 +14,11 @@ Per launch of the render kernel:
   flop_lanes = flop_exec * active_lane_frac: FP32 FLOP done by active lanes
   clock_hz = GRBM_GUI_ACTIVE / 8 XCDs / the kernel's average duration (from
       the kernel-trace stats of the same command)
-usage: make_traffic_json.py SUMMARY.json KEY KERNEL_SUBSTR KERNEL_STATS.csv [OUT]
+  executed_ray_steps_per_launch = config.executed_ray_steps_per_frame of the
+      bench line the same command printed (BENCH_LOG: a file whose last JSON
+      line is bench.py's), so bench.py can price a rank's share of the frame
+      (N > 1) or a walk's poses per executed ray-step
+usage: make_traffic_json.py SUMMARY.json KEY KERNEL_SUBSTR KERNEL_STATS.csv [OUT] [BENCH_LOG]
 """
 import csv
 import json
@@ -22,7 +26,8 @@ import os
 import sys
 
 summ, key, ksub, stats = sys.argv[1:5]
-out = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_counters.json"
+out = sys.argv[5] if len(sys.argv) > 5 and sys.argv[5] else "profiles/pmc_counters.json"
+bench_log = sys.argv[6] if len(sys.argv) > 6 else None
 d = json.load(open(summ))
 k = [n for n in d if ksub in n][0]
 v = d[k]
@@ -44,6 +49,10 @@ if "SQ_THREAD_CYCLES_VALU" in v and "SQ_ACTIVE_INST_VALU" in v:
     entry["active_lane_frac"] = v["SQ_THREAD_CYCLES_VALU"] / (64 * v["SQ_ACTIVE_INST_VALU"])
     if "flop_exec_per_launch" in entry:
         entry["flop_lanes_per_launch"] = entry["flop_exec_per_launch"] * entry["active_lane_frac"]
+if bench_log:
+    line = [ln for ln in open(bench_log) if ln.startswith("{") and '"metric"' in ln][-1]
+    entry["executed_ray_steps_per_launch"] = int(json.loads(line)["config"]["executed_ray_steps_per_frame"])
+    entry["executed_ray_steps_source"] = os.path.relpath(bench_log)
 if "GRBM_GUI_ACTIVE" in v:
     entry["clock_hz"] = v["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9)
 allj = json.load(open(out)) if os.path.exists(out) else {}
