@@ -334,6 +334,9 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 #ifndef RM_SETTLE_T_EVERY
 #define RM_SETTLE_T_EVERY 1  // steps between settle tests (a power of 2)
 #endif
+#ifndef RM_T_BALLOT_SPLIT
+#define RM_T_BALLOT_SPLIT 0
+#endif
 template <bool CAP, int NB, int SM = 0>
 __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                      Tally& cnt) {
@@ -358,7 +361,12 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
         den = upd ? cd : den;
         bool settled = false;
         if constexpr (SM != 0) {
-            if ((it & (RM_SETTLE_T_EVERY - 1)) == 0 && __builtin_amdgcn_ballot_w64((box >= 0.1f) & (h + h >= P)) != 0) {
+#if RM_T_BALLOT_SPLIT  // the two compares' own masks ANDed on the SALU (no 0/1 VGPR and v_cmp_ne per step)
+            const bool any = (__builtin_amdgcn_ballot_w64(box >= 0.1f) & __builtin_amdgcn_ballot_w64(h + h >= P)) != 0;
+#else
+            const bool any = __builtin_amdgcn_ballot_w64((box >= 0.1f) & (h + h >= P)) != 0;
+#endif
+            if ((it & (RM_SETTLE_T_EVERY - 1)) == 0 && any) {
                 const float ax = fabsf(q.x), ay = fabsf(q.y), m = box + 1.0f;
                 const float sx = q.x < 0.0f ? -s.d.x : s.d.x, sy = q.y < 0.0f ? -s.d.y : s.d.y;
                 const float sz = q.z < 0.0f ? -s.d.z : s.d.z;
