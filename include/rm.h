@@ -104,8 +104,9 @@ int rm_abi_version(void);
 /* Create a context on HIP device `device`.  Scene unset, params default. */
 rm_status rm_create(rm_ctx **out, int device);
 /* Waits for the work this context enqueued (its own events, not the device),
- * then frees it.  If the stream it is bound to was destroyed meanwhile (see
- * rm_set_stream), it falls back to waiting for the whole device. */
+ * then frees it.  The stream it is bound to must still exist (rm_set_stream).
+ * If recording on that stream reports an error, it waits for the whole device
+ * instead. */
 rm_status rm_destroy(rm_ctx *ctx);
 
 /* Replaces ShaderLoader::loadFromFile (source/shader_loader.cpp:8-20).
@@ -163,7 +164,10 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *params);
  * Lifetime: a stream must outlive its binding.  Before destroying a stream the
  * context is bound to, bind another one (e.g. rm_set_stream(ctx, NULL)): that
  * records the context's completion events on the old stream while it exists.
- * Streams the context has left may be destroyed at any time. */
+ * Streams the context has left may be destroyed at any time.  Destroying the
+ * bound stream first is undefined behaviour: the HIP runtime does not validate
+ * stream handles, and a later rm_* call (rm_destroy included) that records on
+ * the freed stream crashed the process in a test (SIGSEGV inside libamdhip64). */
 rm_status rm_set_stream(rm_ctx *ctx, void *hip_stream);
 rm_status rm_synchronize(rm_ctx *ctx);
 

@@ -729,9 +729,10 @@ rm_status rm_destroy(rm_ctx *ctx) {
     // nothing this context enqueued still runs: its own events (the streams
     // it left may be the caller's and gone by now); other work on the device
     // is not waited for
-    // A record that fails means the bound stream is gone (destroyed while the
-    // context was still bound to it, against rm.h's rule): the context's work
-    // on it can no longer be waited for by event, so the whole device is.
+    // The bound stream must still exist (rm.h: HIP does not validate stream
+    // handles, so a record on a destroyed one is undefined, not an error).  A
+    // record that does report an error leaves the context's work un-waitable
+    // by event, so the whole device is waited for.
     bool lost = record_sched_last(ctx) != hipSuccess;
     if (ctx->done && ctx->dirty) {
         if (hipEventRecord(ctx->done, ctx->stream) == hipSuccess) (void)hipEventSynchronize(ctx->done);
