@@ -376,6 +376,9 @@ __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
 // margin over what exactness needs; rounding of the extrapolation is ~1e-5.
 // Callers use it to replace whole spans of rays and whole probe sets of a
 // shading point by the plane (PlaneSpan, rm_render_direct.h).
+#ifndef RM_O_ONE_FOLD
+#define RM_O_ONE_FOLD 0
+#endif
 #ifndef RM_O_LBS1  // C5 frame 10.22 -> 10.07 ms (profiles/r03/scene_O_micro_ab.jsonl)
 #define RM_O_LBS1 1
 #endif
@@ -400,6 +403,39 @@ __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n, float& slack
 #endif
     const float mc = sponge_box(q);
     slack = fminf(lbs - (d3 + 0.51f), mc - (d3 + 0.34f));
+#if RM_O_ONE_FOLD
+    // The same three cases as below (the plane; the sponge folded first; the
+    // sphere/cube blend t2 first), with ONE inlined copy of the folds: in a
+    // wave whose lanes fall in different cases the three call sites below each
+    // ran the folds for their lanes.  t2 = T2() is a pure function of p, and
+    // where lbs >= d3 + 0.51 it is d3 bit for bit (h = 0 in both blends), so
+    // t2 is computed before the folds for every lane of a wave that holds a
+    // lane needing it first (one wave-uniform branch, no exec-mask change), and
+    // after them only in a wave that has not computed it and still holds a
+    // folded lane that needs it.  Every lane returns the value of the
+    // expression it returned before.
+    {
+        const bool plane = lbs >= d3 + 0.51f;
+        const float A = fminf(lbs, d3) - 0.0834f;
+        const bool folded = !plane && mc + 0.34f <= A;
+        auto T2 = [&]() {
+            const float d1 = len3<EXACT, true>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
+            const float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
+            return smin_cubic_d<EXACT>(smin_cubic_d<EXACT>(d1, d2, 0.5f, m), d3, 0.5f, m);
+        };
+        float t2 = d3;
+        const bool have_t2 = __builtin_amdgcn_ballot_w64(!plane & !folded) != 0;  // (wave-uniform)
+        if (have_t2) t2 = T2();
+        if (!plane & !folded) n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
+        if (!folded && mc >= t2 + 0.34f) return t2;  // plane lanes: t2 = d3, the plane test
+        const float d0 = sponge_folds<EXACT>(q, mc, n.flop);
+        if (folded && d0 + 0.34f <= A) return d0;
+        if (folded) n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
+        if (!have_t2 && __builtin_amdgcn_ballot_w64(folded) != 0) t2 = T2();
+        n.flop += FL_SMIN;
+        return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
+    }
+#endif
     // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width
     // k = 0.33 (with a margin far above rounding), sminCubic's h is 0 and the
     // result is exactly t2: the sponge's folds are not needed.

@@ -133,6 +133,17 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #ifndef RM_FXAA_TY
 #define RM_FXAA_TY 32
 #endif
+// RM_FXAA_ADDR: span taps addressed without the guard clamps (0.0782 ->
+// 0.0742 ms at 4096^2, same frame; profiles/r05/fxaa_ab.log)
+#ifndef RM_FXAA_ADDR
+#define RM_FXAA_ADDR 1
+#endif
+#ifndef RM_FXAA_RCP_NR
+#define RM_FXAA_RCP_NR 1
+#endif
+#ifndef RM_FXAA_F4
+#define RM_FXAA_F4 0
+#endif
 constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
 constexpr int FXL_MAX_DIM = 1 << 20;
 static_assert((FXL_TY & (FXL_TY - 1)) == 0 && FXL_TY <= 64, "fy_lane: one lane per tile row");
@@ -152,8 +163,17 @@ __device__ __forceinline__ uint32_t unorm8_finite(float c) {
 }
 __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                           int W, int H) {
+#if RM_FXAA_F4
+    // RM_FXAA_F4: each staged texel as the floats GL reads (r, g, b) and its
+    // luma, plus its alpha byte: a span tap is one 16-byte LDS read instead of
+    // a 4-byte read and six unpacking VALU, and a texel is unpacked once per
+    // tile instead of once per tap
+    __shared__ float4 sf4[FXL_H * FXL_W];
+    __shared__ uint8_t salpha[FXL_H * FXL_W];
+#else
     __shared__ uint32_t stex[FXL_H * FXL_W];
     __shared__ float slum[FXL_H * FXL_W];
+#endif
     const int x0 = blockIdx.x * FXL_TX, y0 = blockIdx.y * FXL_TY;
     // output rows y0 .. y0 + TY - 1 read texel rows H-1-y (+-1, span): the block
     // [tx0, tx0 + FXL_W) x [ty0, ty0 + FXL_H), each texel clamped to the frame
@@ -177,12 +197,23 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     for (int k = 0; k < NR; k++) {
         const int r = wv + 4 * k;
         if (r < FXL_H) {
+#if RM_FXAA_F4
+            const RGB c0 = rgb(t0[k]);
+            sf4[r * FXL_W + lane] = make_float4(c0.r, c0.g, c0.b, luma(c0));
+            salpha[r * FXL_W + lane] = (uint8_t)(t0[k] >> 24);
+            if (lane < FXL_W - 64) {
+                const RGB c1 = rgb(t1[k]);
+                sf4[r * FXL_W + 64 + lane] = make_float4(c1.r, c1.g, c1.b, luma(c1));
+                salpha[r * FXL_W + 64 + lane] = (uint8_t)(t1[k] >> 24);
+            }
+#else
             stex[r * FXL_W + lane] = t0[k];
             slum[r * FXL_W + lane] = luma(rgb(t0[k]));
             if (lane < FXL_W - 64) {
                 stex[r * FXL_W + 64 + lane] = t1[k];
                 slum[r * FXL_W + 64 + lane] = luma(rgb(t1[k]));
             }
+#endif
         }
     }
     __syncthreads();
@@ -193,11 +224,33 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     const float fx = ((float)x + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
     // a span tap: post.frag's float address (NEAREST), then the staged texel
     // (block row * FXL_W as a 24-bit multiply: the row is clamped into the block)
+#if RM_FXAA_F4
+    const int blk0 = -(ty0 * FXL_W + tx0);  // (the bound above keeps every span texel inside the block)
+    auto span_tap = [&](float u, float v) -> RGB {
+        const float4 t = sf4[__mul24(floor_i32(v * (float)H), FXL_W) + floor_i32(u * (float)W) + blk0];
+        return RGB{t.x, t.y, t.z};
+    };
+#elif RM_FXAA_ADDR
+    // (the bound above keeps every span texel inside the block, so no clamp:
+    // the block index is one signed 24-bit multiply-add of the texel
+    // coordinates and a wave-uniform offset; an LDS read outside the
+    // workgroup's allocation returns 0 on this hardware in any case)
+    const int blk4 = -4 * (ty0 * FXL_W + tx0);  // (byte offsets)
+    auto span_tap = [&](float u, float v) -> RGB {
+        // byte offset 4 gx + (296 gy + blk4): v_mad_i32_i24 + v_lshl_add_u32 (left
+        // to itself the compiler forms mul + shift + add3)
+        const int row = __mul24(floor_i32(v * (float)H), 4 * FXL_W) + blk4;
+        int a;
+        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(floor_i32(u * (float)W)), "v"(row));
+        return rgb(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(stex) + a));
+    };
+#else
     auto span_tap = [&](float u, float v) -> RGB {
         const int gx = clamp_to(floor_i32(u * (float)W) - tx0, FXL_W - 1);
         const int gy = clamp_to(floor_i32(v * (float)H) - ty0, FXL_H - 1);
         return rgb(stex[__umul24(gy, FXL_W) + gx]);
     };
+#endif
     // fy of row y0 + l in lane l (rows past the frame: the clamped row), one
     // correctly rounded division per tile instead of one per row; a row reads
     // its lane's value as a wave-uniform scalar
@@ -207,16 +260,34 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     auto pixel = [&](int ly) -> uint32_t {
         const int y = min(y0 + ly, H - 1);
         const int m = (FXL_TY - 1 - (y - y0) + FXL_HALO) * FXL_W + (lane + FXL_HALO);
+#if RM_FXAA_F4
+        const float lNW = sf4[m - FXL_W - 1].w, lNE = sf4[m - FXL_W + 1].w, lSW = sf4[m + FXL_W - 1].w;
+        const float lSE = sf4[m + FXL_W + 1].w, lM = sf4[m].w;
+        const uint32_t tM = (uint32_t)salpha[m] << 24;
+#else
         const float lNW = slum[m - FXL_W - 1], lNE = slum[m - FXL_W + 1], lSW = slum[m + FXL_W - 1];
         const float lSE = slum[m + FXL_W + 1], lM = slum[m];
         const uint32_t tM = stex[m];
+#endif
         const float fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_lane), ly));
         const float lMin = fminf(lM, fminf(fminf(lNW, lNE), fminf(lSW, lSE)));
         const float lMax = fmaxf(lM, fmaxf(fmaxf(lNW, lNE), fmaxf(lSW, lSE)));
         float dx = -((lNW + lNE) - (lSW + lSE));
         float dy = ((lNW + lSW) - (lNE + lSE));
         float dirReduce = fmaxf((lNW + lNE + lSW + lSE) * (0.25f * FXAA_REDUCE_MUL), FXAA_REDUCE_MIN);
+#if RM_FXAA_RCP_NR
+        // 1/x correctly rounded as one Newton step from v_rcp_f32: x lies in
+        // [1/128, 2.125] (dirReduce in [1/128, 1/8], |dx|, |dy| <= 2 for lumas
+        // in [0, 1]), and over every float of [2^-8, 4) the step equals the IEEE
+        // quotient bit for bit on gfx950 (tools/rcp_exhaustive.hip: 83,886,080
+        // floats, 0 mismatches; profiles/r05/rcp_exhaustive.json): 3 VALU
+        // instead of the 12 of the div_scale / div_fmas / div_fixup expansion
+        const float dmin = fminf(fabsf(dx), fabsf(dy)) + dirReduce;
+        const float r0 = __builtin_amdgcn_rcpf(dmin);
+        float rcpDirMin = fmaf(fmaf(-dmin, r0, 1.0f), r0, r0);
+#else
         float rcpDirMin = 1.0f / (fminf(fabsf(dx), fabsf(dy)) + dirReduce);
+#endif
         dx = __builtin_amdgcn_fmed3f(dx * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX) * ivx;
         dy = __builtin_amdgcn_fmed3f(dy * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX) * ivy;
         RGB s1 = span_tap(fx + dx * k1, fy + dy * k1);
@@ -443,6 +514,10 @@ __device__ __forceinline__ void vload_cell(const float* base, int cell, f8v& c8,
     c4 = f4v{q2.x, q2.y, q2.z, q2.w};
 }
 
+#ifndef RM_BLOOM_V2
+#define RM_BLOOM_V2 0
+#endif
+#if !RM_BLOOM_V2
 // bloom.frag:33-43 for lod > 0 (minification: levels d1, d2 blended by fr).
 // One wave per 8x8-pixel tile, 2x2 waves per workgroup.  A tap's value is
 // its cell's polynomial; a level texel spans 2^d1 >= 0.025 H pixels, so the
@@ -504,6 +579,99 @@ __global__ __launch_bounds__(256) void rm_bloom_min_kernel(Level L0, Cells A, Ce
                 color.b + gmax_(bl.b - 0.3f, 0.0f)};
     out[(size_t)y * W + x] = unorm8(color.r) | (unorm8(color.g) << 8) | (unorm8(color.b) << 16) | (255u << 24);
 }
+#endif
+
+#if RM_BLOOM_V2
+// rm_bloom_min_kernel, restructured (RM_BLOOM_V2): the same taps, products and
+// multiply-adds in the same order per lane (bit-identical), with
+//  * the row's three Gaussian weights chosen by scalar selects (no load per
+//    tap) and copied to VGPRs once per row (the c00 g term's operand), and the
+//    products g b shared by the symmetric taps of a row (g[i] = g[4-i]);
+//  * a row whose ten cells (5 taps x 2 levels) are all wave-uniform -- most
+//    rows -- runs without a branch per tap, so the compiler schedules its
+//    scalar loads ahead of the arithmetic; other rows branch per tap as before;
+//  * the wave-uniform cells read by compiler-scheduled scalar loads from the
+//    constant address space instead of an asm block that waited on each tap.
+typedef const __attribute__((address_space(4))) float* cfloat_p;
+__device__ __forceinline__ void sload_cell(const float* base, int off_bytes, f8v& c8, f4v& c4) {
+    cfloat_p p = (cfloat_p)(const void*)base;
+    const int o = __builtin_amdgcn_readfirstlane(off_bytes) >> 2;
+    c8 = f8v{p[o], p[o + 1], p[o + 2], p[o + 3], p[o + 4], p[o + 5], p[o + 6], p[o + 7]};
+    c4 = f4v{p[o + 8], p[o + 9], p[o + 10], p[o + 11]};
+}
+__global__ __launch_bounds__(256) void rm_bloom_min_kernel(Level L0, Cells A, Cells B, uint32_t* __restrict__ out,
+                                                           int W, int H, float fr) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7), y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
+    if (x >= W || y >= H) return;
+    const float u = ((float)x + 0.5f) / (float)W, v = 1.0f - ((float)y + 0.5f) / (float)H;  // bloom.frag:36
+    RGB color = tex_bilinear(L0, u, v);
+    const float scale = 0.05f, iaspect = (float)H / (float)W;
+    CAxis xa[5], xb[5];
+    int sxa[5], sxb[5];
+    bool ux[5], allx = true;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const float uu = u + ((float)(i - 2) * iaspect) * scale;
+        xa[i] = caxis(uu, A.w);
+        xb[i] = caxis(uu, B.w);
+        const bool ua = wave_uniform(xa[i].c, sxa[i]), ub = wave_uniform(xb[i].c, sxb[i]);
+        ux[i] = ua && ub;
+        allx = allx && ux[i];
+        sxa[i] *= kCellFloats * 4;
+        sxb[i] *= kCellFloats * 4;
+    }
+    RGB ba{0.0f, 0.0f, 0.0f}, bb{0.0f, 0.0f, 0.0f};
+#pragma unroll 1
+    for (int j = 0; j < 5; j++) {  // (rolled: one row's cells and weights live at a time)
+        const float vv = v + (float)(j - 2) * scale;
+        const CAxis ya = caxis(vv, A.h), yb = caxis(vv, B.h);
+        int sya, syb;
+        const bool uya = wave_uniform(ya.c, sya), uyb = wave_uniform(yb.c, syb);
+        const bool uy = uya && uyb;
+        sya *= (A.w + 1) * kCellFloats * 4;
+        syb *= (B.w + 1) * kCellFloats * 4;
+        // kGauss[|i - 2|][|j - 2|] of this row (scalar selects)
+        const int jr = j < 2 ? 2 - j : j - 2;
+        const float g0 = jr == 0 ? 41.0f / 273.0f : jr == 1 ? 26.0f / 273.0f : 7.0f / 273.0f;
+        const float g1 = jr == 0 ? 26.0f / 273.0f : jr == 1 ? 16.0f / 273.0f : 4.0f / 273.0f;
+        const float g2 = jr == 0 ? 7.0f / 273.0f : jr == 1 ? 4.0f / 273.0f : 1.0f / 273.0f;
+        const float gi[5] = {g2, g1, g0, g1, g2};
+        if (uy && allx) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                f8v a8, b8;
+                f4v a4, b4;
+                sload_cell(A.p, sya + sxa[i], a8, a4);
+                sload_cell(B.p, syb + sxb[i], b8, b4);
+                cell_acc(a8, a4, xa[i].f, ya.f, gi[i], ba);
+                cell_acc(b8, b4, xb[i].f, yb.f, gi[i], bb);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                f8v a8, b8;
+                f4v a4, b4;
+                if (uy & ux[i]) {  // (as rm_bloom_min_kernel: SGPR operands stay SGPRs)
+                    sload_cells(A.p, sya + sxa[i], B.p, syb + sxb[i], a8, a4, b8, b4);
+                    cell_acc(a8, a4, xa[i].f, ya.f, gi[i], ba);
+                    cell_acc(b8, b4, xb[i].f, yb.f, gi[i], bb);
+                } else {
+                    vload_cell(A.p, ya.c * (A.w + 1) + xa[i].c, a8, a4);
+                    vload_cell(B.p, yb.c * (B.w + 1) + xb[i].c, b8, b4);
+                    cell_acc(a8, a4, xa[i].f, ya.f, gi[i], ba);
+                    cell_acc(b8, b4, xb[i].f, yb.f, gi[i], bb);
+                }
+            }
+        }
+    }
+    const float ifr = 1.0f - fr;
+    const RGB bl{ifr * ba.r + fr * bb.r, ifr * ba.g + fr * bb.g, ifr * ba.b + fr * bb.b};
+    color = RGB{color.r + gmax_(bl.r - 0.3f, 0.0f), color.g + gmax_(bl.g - 0.3f, 0.0f),
+                color.b + gmax_(bl.b - 0.3f, 0.0f)};
+    out[(size_t)y * W + x] = unorm8(color.r) | (unorm8(color.g) << 8) | (unorm8(color.b) << 16) | (255u << 24);
+}
+#endif
 
 BloomPlan bloom_plan(int W, int H) {
     BloomPlan p{};

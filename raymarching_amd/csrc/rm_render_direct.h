@@ -55,6 +55,11 @@ __device__ __forceinline__ V3 mnormalize(V3 a) {
 // plane-only when the slack there is >= 2.05.
 template <int SC>
 constexpr bool kPlaneSpans = SC == SCENE_O || SC == SCENE_OG;
+// RM_O_SPANS=0 (analysis only: the structural share of the plugin gap, DESIGN.md
+// 2.4) keeps scene O's code shape but never takes a plane span or plane probe set
+#ifndef RM_O_SPANS
+#define RM_O_SPANS 1
+#endif
 __device__ __forceinline__ float plane_rate(V3 d) {  // (v_rcp: 1 ulp is far inside the margin)
     return __builtin_amdgcn_rcpf(1.01f + fabsf(d.y));
 }
@@ -64,7 +69,7 @@ __device__ __forceinline__ bool plane_probes(const FrameConst& F, V3 p) {
         Tally scratch;  // (not a ray-step of the reference)
         float slack;
         (void)scene_dist_O<false>(p, sponge_space<false>(F, p), scratch, slack);
-        return slack >= 2.05f;
+        return RM_O_SPANS && slack >= 2.05f;
     } else {
         (void)F; (void)p;
         return false;
@@ -120,7 +125,7 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
                 float slack;
                 cnt.flop += FL_TRANSFORM;
                 res = scene_dist_O<true>(q, sponge_space<true>(F, q), cnt, slack);
-                t_plane = depth + slack * ia;
+                t_plane = RM_O_SPANS ? depth + slack * ia : 0.0f;
             }
             last = depth;
             if (INSIDE) {
@@ -254,7 +259,7 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
             float slack;
             cnt.flop += FL_LINRAY;
             h = scene_dist_O<false>(at(w, t), at(s, t), cnt, slack);
-            t_plane = t + slack * ia;
+            t_plane = RM_O_SPANS ? t + slack * ia : 0.0f;
         }
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
@@ -334,8 +339,12 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 #ifndef RM_SETTLE_T_EVERY
 #define RM_SETTLE_T_EVERY 1  // steps between settle tests (a power of 2)
 #endif
+// RM_T_BALLOT_SPLIT: the settle gate as the AND of the two compares' own
+// masks (s_and_b64) instead of a ballot of their combined i1, which the
+// backend materialized as a 0/1 VGPR and a v_cmp_ne per step: 2 VALU fewer per
+// shadow step, C3 0.4603-0.4626 -> 0.4527-0.4549 ms (profiles/r05/ab_settle_T.log)
 #ifndef RM_T_BALLOT_SPLIT
-#define RM_T_BALLOT_SPLIT 0
+#define RM_T_BALLOT_SPLIT 1
 #endif
 template <bool CAP, int NB, int SM = 0>
 __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const LinRay& s, float mint, float maxt,

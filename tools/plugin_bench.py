@@ -23,12 +23,15 @@ def main():
     ap.add_argument("--max-steps", type=int, default=512)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--pose", default="P0")
+    ap.add_argument("--cases", default="", help="comma-separated case-name prefixes (default: all)")
     a = ap.parse_args()
     import torch
     r = rm.Renderer(0)
     pose = rm.POSES[a.pose]
     out = torch.empty((a.size, a.size), dtype=torch.int32, device="cuda:0")
     for name, f in CASES:
+        if a.cases and not any(name.startswith(c) for c in a.cases.split(",")):
+            continue
         path = f if f.endswith(".frag") else os.path.join(rm.SCENES_DIR, f)
         t0 = time.time()
         r.load_scene(path)
@@ -38,12 +41,16 @@ def main():
         _, st = r.render_rgba8(a.size, a.size, out=out, stats=True)
         evals = st["evals"]
         r.set_params(count_evals=0)
+        t_end = time.time() + 0.3  # clock ramp, and the adaptive order settles
+        while time.time() < t_end:
+            r.render_rgba8(a.size, a.size, out=out)
+        torch.cuda.synchronize()
         ms = []
         for _ in range(a.reps):
             _, st = r.render_rgba8(a.size, a.size, out=out, stats=True)
             ms.append(st["kernel_ms"])
-        best = min(ms)
-        print(json.dumps(dict(case=name, file=f, size=a.size, max_steps=a.max_steps, pose=a.pose,
+        best = sorted(ms)[len(ms) // 2]  # (median)
+        print(json.dumps(dict(lib=os.path.basename(os.environ.get("RM_LIB", "librm.so")), case=name, file=f, size=a.size, max_steps=a.max_steps, pose=a.pose,
                               load_s=round(load_s, 3), kernel_ms=round(best, 4), kernel_ms_all=[round(x, 4) for x in ms],
                               evals=evals, ray_steps_per_s=evals / (best * 1e-3))), flush=True)
     r.close()
