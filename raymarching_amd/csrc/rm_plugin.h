@@ -22,28 +22,27 @@
 namespace rm {
 namespace glsl {
 
-// The pass's uniforms, copied at the start of every plugin kernel from its
-// FrameConst argument into LDS, where any function of the scene can read
-// them (the kernel-argument segment is addressable only in the kernel's own
-// body, and hiprtc does not inline every call).
-struct PluginUniforms {
-    float res_x, res_y, pos_x, pos_y, pos_z, mouse_x, mouse_y, time;
-};
-__shared__ PluginUniforms plugin_lds_uniforms;
-
-__device__ __forceinline__ void plugin_bind_uniforms(const FrameConst& F) {
-    if (threadIdx.x == 0)
-        plugin_lds_uniforms = PluginUniforms{F.res_x, F.res_y, F.pos_x, F.pos_y, F.pos_z, F.mouse_x, F.mouse_y, F.time};
-    __syncthreads();
+// The pass's uniforms, read where a scene function needs them from the
+// kernel's own FrameConst argument: every plugin kernel takes it first, so it
+// sits at offset 0 of the kernel-argument segment, and the scene's functions
+// are force-inlined into the kernels (rm_plugin_host.cpp), where that segment
+// is addressable.  These are constant-address-space loads, invariant, so a
+// uniform read inside a march loop -- transformR's sin and cos of u_time --
+// is hoisted out of it.  (Round 4 copied the uniforms to LDS; the LDS read of
+// u_time stayed inside the loops, whose volatile asm statements LLVM must
+// assume to write memory, and the scene-O plugin evaluated two sin and two
+// cos, with two IEEE divisions, on every ray-step.)
+typedef const __attribute__((address_space(4))) FrameConst* KernargFrame;
+__device__ __forceinline__ KernargFrame plugin_frame() {
+    return (KernargFrame)__builtin_amdgcn_kernarg_segment_ptr();
 }
-__device__ __forceinline__ const PluginUniforms& plugin_uniforms() { return plugin_lds_uniforms; }
 
 }  // namespace glsl
 }  // namespace rm
 
-#define u_resolution (::rm::glsl::vec2(::rm::glsl::plugin_uniforms().res_x, ::rm::glsl::plugin_uniforms().res_y))
-#define u_pos                                                                                            \
-    (::rm::glsl::vec3(::rm::glsl::plugin_uniforms().pos_x, ::rm::glsl::plugin_uniforms().pos_y,          \
-                      ::rm::glsl::plugin_uniforms().pos_z))
-#define u_mouse (::rm::glsl::vec2(::rm::glsl::plugin_uniforms().mouse_x, ::rm::glsl::plugin_uniforms().mouse_y))
-#define u_time (::rm::glsl::plugin_uniforms().time)
+#define u_resolution (::rm::glsl::vec2(::rm::glsl::plugin_frame()->res_x, ::rm::glsl::plugin_frame()->res_y))
+#define u_pos                                                                                              \
+    (::rm::glsl::vec3(::rm::glsl::plugin_frame()->pos_x, ::rm::glsl::plugin_frame()->pos_y,               \
+                      ::rm::glsl::plugin_frame()->pos_z))
+#define u_mouse (::rm::glsl::vec2(::rm::glsl::plugin_frame()->mouse_x, ::rm::glsl::plugin_frame()->mouse_y))
+#define u_time (::rm::glsl::plugin_frame()->time)

@@ -195,9 +195,14 @@ std::string translation_unit(const std::string& src, const std::string& file) {
     return "#include \"rm_plugin.h\"\n"
            "namespace rm {\nnamespace glsl {\nnamespace {\n"
            "#pragma clang force_cuda_host_device begin\n"
+           // (every scene function inlined into the kernels: the uniforms are
+           // read from the kernel-argument segment, rm_plugin.h; GLSL has no
+           // recursion)
+           "#pragma clang attribute push (__attribute__((always_inline)), apply_to = function)\n"
            "#line 1 \"" + name + "\"\n" +
            glsl_source(src) +
-           "\n#pragma clang force_cuda_host_device end\n"
+           "\n#pragma clang attribute pop\n"
+           "#pragma clang force_cuda_host_device end\n"
            "}  // namespace\n}  // namespace glsl\n}  // namespace rm\n"
            "#include \"rm_plugin_kernels.h\"\n";
 }

@@ -31,7 +31,6 @@ template <bool COUNT>
 __device__ __forceinline__ void plugin_render_tile(const FrameConst& F, void* out, int rgba8,
                                                    unsigned long long* evals) {
     const uint64_t t_start = F.tile_cost ? clock64() : 0;
-    glsl::plugin_bind_uniforms(F);
     const int lane = threadIdx.x;
     int bx = blockIdx.x, by = blockIdx.y;
     if (F.tile_order) {  // costliest tiles first (rm_params.schedule, rm_set_tile_order)
@@ -84,6 +83,5 @@ extern "C" __global__ __launch_bounds__(64) void rm_plugin_render_count(rm::Fram
 // sceneSDF(p) at explicit points (rm_scene_eval)
 extern "C" __global__ __launch_bounds__(256) void rm_plugin_eval(rm::FrameConst F, const float* pts, long long n,
                                                                  float* dist, float* mat) {
-    rm::glsl::plugin_bind_uniforms(F);
     rm::scene_eval_one<rm::SCENE_PLUGIN>(F, pts, n, dist, mat);
 }

@@ -514,76 +514,13 @@ __device__ __forceinline__ void vload_cell(const float* base, int cell, f8v& c8,
     c4 = f4v{q2.x, q2.y, q2.z, q2.w};
 }
 
-#ifndef RM_BLOOM_V2
-#define RM_BLOOM_V2 0
-#endif
-#if !RM_BLOOM_V2
 // bloom.frag:33-43 for lod > 0 (minification: levels d1, d2 blended by fr).
 // One wave per 8x8-pixel tile, 2x2 waves per workgroup.  A tap's value is
 // its cell's polynomial; a level texel spans 2^d1 >= 0.025 H pixels, so the
-// lanes of a wave nearly always share a tap's cell on both levels: the two
-// cells are fetched once per wave into SGPRs (otherwise per lane).  The
-// Gaussian sums of the two levels are blended once at the end (oracle
-// bloom_pixel).  31 VALU per tap.
-__global__ __launch_bounds__(256) void rm_bloom_min_kernel(Level L0, Cells A, Cells B, uint32_t* __restrict__ out,
-                                                           int W, int H, float fr) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7), y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
-    if (x >= W || y >= H) return;
-    const float u = ((float)x + 0.5f) / (float)W, v = 1.0f - ((float)y + 0.5f) / (float)H;  // bloom.frag:36
-    RGB color = tex_bilinear(L0, u, v);
-    const float scale = 0.05f, iaspect = (float)H / (float)W;
-    CAxis xa[5], xb[5];
-    int sxa[5], sxb[5];
-    bool ux[5];
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-        const float uu = u + ((float)(i - 2) * iaspect) * scale;
-        xa[i] = caxis(uu, A.w);
-        xb[i] = caxis(uu, B.w);
-        const bool ua = wave_uniform(xa[i].c, sxa[i]), ub = wave_uniform(xb[i].c, sxb[i]);
-        ux[i] = ua && ub;
-        sxa[i] *= kCellFloats * 4;
-        sxb[i] *= kCellFloats * 4;
-    }
-    RGB ba{0.0f, 0.0f, 0.0f}, bb{0.0f, 0.0f, 0.0f};
-#pragma unroll 1
-    for (int j = 0; j < 5; j++) {  // (rolled: one row's cells and weights live at a time)
-        const float vv = v + (float)(j - 2) * scale;
-        const CAxis ya = caxis(vv, A.h), yb = caxis(vv, B.h);
-        int sya, syb;
-        const bool uya = wave_uniform(ya.c, sya), uyb = wave_uniform(yb.c, syb);
-        const bool uy = uya && uyb;
-        sya *= (A.w + 1) * kCellFloats * 4;
-        syb *= (B.w + 1) * kCellFloats * 4;
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-            const float g = kGauss[i < 2 ? 2 - i : i - 2][j < 2 ? 2 - j : j - 2];
-            f8v a8, b8;
-            f4v a4, b4;
-            if (uy & ux[i]) {  // (the arithmetic in each branch: SGPR operands stay SGPRs)
-                sload_cells(A.p, sya + sxa[i], B.p, syb + sxb[i], a8, a4, b8, b4);
-                cell_acc(a8, a4, xa[i].f, ya.f, g, ba);
-                cell_acc(b8, b4, xb[i].f, yb.f, g, bb);
-            } else {
-                vload_cell(A.p, ya.c * (A.w + 1) + xa[i].c, a8, a4);
-                vload_cell(B.p, yb.c * (B.w + 1) + xb[i].c, b8, b4);
-                cell_acc(a8, a4, xa[i].f, ya.f, g, ba);
-                cell_acc(b8, b4, xb[i].f, yb.f, g, bb);
-            }
-        }
-    }
-    const float ifr = 1.0f - fr;
-    const RGB bl{ifr * ba.r + fr * bb.r, ifr * ba.g + fr * bb.g, ifr * ba.b + fr * bb.b};
-    color = RGB{color.r + gmax_(bl.r - 0.3f, 0.0f), color.g + gmax_(bl.g - 0.3f, 0.0f),
-                color.b + gmax_(bl.b - 0.3f, 0.0f)};
-    out[(size_t)y * W + x] = unorm8(color.r) | (unorm8(color.g) << 8) | (unorm8(color.b) << 16) | (255u << 24);
-}
-#endif
-
-#if RM_BLOOM_V2
-// rm_bloom_min_kernel, restructured (RM_BLOOM_V2): the same taps, products and
-// multiply-adds in the same order per lane (bit-identical), with
+// lanes of a wave mostly share a tap's cell on both levels: the two cells are
+// then read once per wave into SGPRs (otherwise per lane).  The Gaussian sums
+// of the two levels are blended once at the end (oracle bloom_pixel).
+// Round 5 (0.488 -> 0.444 ms at 4096^2, bit-identical; profiles/r05/bloom_ab.log):
 //  * the row's three Gaussian weights chosen by scalar selects (no load per
 //    tap) and copied to VGPRs once per row (the c00 g term's operand), and the
 //    products g b shared by the symmetric taps of a row (g[i] = g[4-i]);
@@ -599,8 +536,11 @@ __device__ __forceinline__ void sload_cell(const float* base, int off_bytes, f8v
     c8 = f8v{p[o], p[o + 1], p[o + 2], p[o + 3], p[o + 4], p[o + 5], p[o + 6], p[o + 7]};
     c4 = f4v{p[o + 8], p[o + 9], p[o + 10], p[o + 11]};
 }
-__global__ __launch_bounds__(256) void rm_bloom_min_kernel(Level L0, Cells A, Cells B, uint32_t* __restrict__ out,
-                                                           int W, int H, float fr) {
+#ifndef RM_BLOOM_WAVES  // minimum waves per SIMD for the register allocator (1 = unconstrained)
+#define RM_BLOOM_WAVES 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BLOOM_WAVES))) void rm_bloom_min_kernel(
+    Level L0, Cells A, Cells B, uint32_t* __restrict__ out, int W, int H, float fr) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7), y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
     if (x >= W || y >= H) return;
@@ -671,7 +611,6 @@ __global__ __launch_bounds__(256) void rm_bloom_min_kernel(Level L0, Cells A, Ce
                 color.b + gmax_(bl.b - 0.3f, 0.0f)};
     out[(size_t)y * W + x] = unorm8(color.r) | (unorm8(color.g) << 8) | (unorm8(color.b) << 16) | (255u << 24);
 }
-#endif
 
 BloomPlan bloom_plan(int W, int H) {
     BloomPlan p{};
