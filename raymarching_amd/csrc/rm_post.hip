@@ -536,11 +536,8 @@ __device__ __forceinline__ void sload_cell(const float* base, int off_bytes, f8v
     c8 = f8v{p[o], p[o + 1], p[o + 2], p[o + 3], p[o + 4], p[o + 5], p[o + 6], p[o + 7]};
     c4 = f4v{p[o + 8], p[o + 9], p[o + 10], p[o + 11]};
 }
-#ifndef RM_BLOOM_WAVES  // minimum waves per SIMD for the register allocator (1 = unconstrained)
-#define RM_BLOOM_WAVES 1
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BLOOM_WAVES))) void rm_bloom_min_kernel(
-    Level L0, Cells A, Cells B, uint32_t* __restrict__ out, int W, int H, float fr) {
+__global__ __launch_bounds__(256) void rm_bloom_min_kernel(Level L0, Cells A, Cells B, uint32_t* __restrict__ out,
+                                                           int W, int H, float fr) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7), y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
     if (x >= W || y >= H) return;

@@ -237,9 +237,9 @@ __device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& 
 // in cnt.skipped); O/OG only.  The settle test (~45 VALU) runs on every
 // RM_SETTLE_O_EVERY-th step: C5 frame 11.25 -> 10.51 ms with 8, 10.79 with 4
 // (profiles/r03/scene_O_settle_ab.jsonl).
-template <int SC, int SM = 0>
-__device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
-                                              Tally& cnt) {
+template <int SC, int SM = 0, bool CAP = true>
+__device__ __forceinline__ float soft_shadow2_loop(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
+                                                   Tally& cnt) {
     constexpr bool kSettle = kPlaneSpans<SC> && SM != 0 && RM_SETTLE_O;
     const LinRay w{ro, rd}, s = sponge_ray(F, ro, rd);
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
@@ -290,12 +290,28 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
         }
 #if RM_O_SHADOW_EXIT2
         if ((h < 0.001f) | !(t < maxt)) break;
-        if (it >= F.shadow_max_steps) break;  // (wave-uniform)
+        if (CAP && it >= F.shadow_max_steps) break;  // (wave-uniform)
 #else
-        if ((h < 0.001f) | !(t < maxt) | settled | (it >= F.shadow_max_steps)) break;
+        if ((h < 0.001f) | !(t < maxt) | settled | (CAP && it >= F.shadow_max_steps)) break;
 #endif
     }
     return h < 0.001f ? 0.0f : sqrtf(16.0f * num / den);
+}
+// RM_O_SHADOW_UNCAPPED: the reference's uncapped march (the default) as a loop
+// copy without the step-cap test, as scene T's (soft_shadow2_T).  Round 3
+// measured no gain while the kernel spilled; without spills: C5 frame
+// 8.524 -> 8.510 ms, C5 share 1.082 -> 1.077, O 4096^2 2.219 -> 2.212, frames
+// identical (profiles/r05/ab_O_uncapped.jsonl)
+#ifndef RM_O_SHADOW_UNCAPPED
+#define RM_O_SHADOW_UNCAPPED 1
+#endif
+template <int SC, int SM = 0>
+__device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
+                                              Tally& cnt) {
+#if RM_O_SHADOW_UNCAPPED
+    if (F.shadow_max_steps == __INT_MAX__) return soft_shadow2_loop<SC, SM, false>(F, ro, rd, mint, maxt, cnt);
+#endif
+    return soft_shadow2_loop<SC, SM, true>(F, ro, rd, mint, maxt, cnt);
 }
 
 // softShadow2 for scene T (fast math), stepping in sponge space and free of
@@ -415,8 +431,7 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
 // The uncapped loop (the reference's, and the default) carries no step
 // counter: a uniform counter test merged into the lanes' exit mask costs 5
 // SALU per step, and SALU issue is a co-bottleneck of the kernel.
-// (Scene O's soft_shadow2 measured no gain from the same split: its kernel
-// spills at occupancy 8 and the second loop copy spilled more.)
+// (Scene O's soft_shadow2 has the same split since round 5: RM_O_SHADOW_UNCAPPED.)
 #ifndef RM_SHADOW_SETTLE
 #define RM_SHADOW_SETTLE 1
 #endif
