@@ -534,7 +534,10 @@ __device__ __forceinline__ vec3 mengersponge(vec3 p) {
         // fold m yields c = (min(da, db, dc) - 1) / s <= 1/s (r <= 2), so once
         // d >= RN(1/s) no later fold can win `c > d`: an exact early exit
         // (rm_device.h sponge_folds), which skips the folds far from the sponge
-        if (!(d < 1.0f / (s * 3.0f))) break;
+        // (wave-uniform, as rm_device.h sponge_folds: a fold runs while any lane
+        // needs it, and leaves d and res unchanged on the lanes past their exit;
+        // a per-lane break was if-converted, every fold computed on every call)
+        if (__builtin_amdgcn_ballot_w64(d < 1.0f / (s * 3.0f)) == 0) break;
         vec3 a = mod(p * s, 2.0f) - 1.0f;
         s *= 3.0f;
         vec3 r = abs(1.0f - 3.0f * abs(a));
