@@ -407,6 +407,7 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, const RowPart &part, int n
     F.rx_c = rm::glsl_cos(ax); F.rx_s = rm::glsl_sin(ax);
     F.W = W; F.H = H;
     F.cycle = part.cycle; F.offset = part.offset; F.run = part.run; F.nrows = nrows;
+    F.run_magic = rm::div_magic((uint32_t)part.run, (uint64_t)H + 1);  // packed rows j < H
     F.time = c->time;
     F.mouse_x = c->mouse[0];
     F.mouse_y = c->mouse[1];

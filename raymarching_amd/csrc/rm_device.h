@@ -65,7 +65,21 @@ struct FrameConst {
     float sample_part;             // u_sample_part
     float jit_x, jit_y;            // with accumulate: sub-pixel offset of the fragment, fract(u_seed1) - 0.5
     uint32_t* persist;             // KERNEL_PERSIST: {next dispatch ordinal, waves done}, zero between launches
+    uint32_t run_magic;            // floor(j / run) = umulhi(j, run_magic) for every packed row j, or 0: divide
+    uint32_t gx_magic;             // floor(t / tiles_x) = umulhi(t, gx_magic) for every tile t, or 0: divide
 };
+
+// Division by a per-launch divisor d (host: div_magic): with m = floor(2^32 / d)
+// + 1 = (2^32 + e) / d, e in [1, d], a m / 2^32 = a / d + a e / (d 2^32), which
+// stays below the next integer while a e < 2^32; the host sets m only when
+// every dividend a of the launch has a d < 2^32 (and d >= 2): one v_mul_hi_u32
+// instead of the ~12 VALU of an integer division by a run-time value.
+__host__ __device__ inline uint32_t div_magic(uint32_t d, uint64_t a_end) {
+    return d >= 2 && a_end * (uint64_t)d < (1ull << 32) ? (uint32_t)((1ull << 32) / d + 1) : 0u;
+}
+__device__ __forceinline__ int div_by(int a, uint32_t m, int d) {
+    return m ? (int)__umulhi((uint32_t)a, m) : a / d;
+}
 
 // Buckets of the adaptive dispatch order (rm_capi.cpp, rm_kernels.hip): 256
 // logarithmic buckets of a tile's duration, 8 per octave of shader clocks
@@ -584,9 +598,15 @@ __device__ __forceinline__ float gpow(float x, float y) {
     if constexpr (FAST) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
     else return powf(x, y);
 }
+// RM_FAST_SHADE (scenes S0/T, FAST): the colour path's division and exp as
+// the hardware reciprocal and exp2 (1 ulp; the colour is smooth in them):
+// arcp division had compiled to a frexp/ldexp-scaled reciprocal, 8 VALU each
+#ifndef RM_FAST_SHADE
+#define RM_FAST_SHADE 1
+#endif
 template <bool FAST>
 __device__ __forceinline__ float tonemap1(float c, float e2) {
-    float col = c * 2.0f / (1.0f + c);
+    float col = FAST && RM_FAST_SHADE ? (c * 2.0f) * __builtin_amdgcn_rcpf(1.0f + c) : c * 2.0f / (1.0f + c);
     if constexpr (FAST) {  // pow(pow(x, .4545), e2) = exp2(.4545 e2 log2 x): one log2, one exp2
         col = __builtin_amdgcn_exp2f((0.4545f * e2) * __builtin_amdgcn_logf(col));
     } else {
@@ -610,9 +630,10 @@ __device__ __forceinline__ V3 post_colour(V3 c, float v) {
 }
 
 // common.frag:1032-1042 with be = bi = vec3(2) and the fog colour of the scenes
+template <bool FAST = false>
 __device__ __forceinline__ V3 apply_scattering(V3 color, V3 ro, V3 p) {
     float d = 1.0f - clamp01(length(p - ro) / ZFAR);
-    float e = expf(-d * 2.0f);
+    float e = FAST && RM_FAST_SHADE ? __builtin_amdgcn_exp2f(d * -2.8853900817779268f) : expf(-d * 2.0f);  // 2 log2(e)
     return color * (1.0f - e) + v3(0.34f, 0.435f, 0.57f) * e;
 }
 // output_shader.frag:178-182

@@ -55,8 +55,10 @@ template <int SC, int K, typename OUT>
 hipError_t launch_direct(const FrameConst& F, OUT* out, unsigned long long* evals, hipStream_t s) {
     using T = Tiling<K>;
     dim3 grid((F.W + T::TW - 1) / T::TW, (F.nrows + T::TH - 1) / T::TH), block(64 * T::WPB);
-    if (evals) hipLaunchKernelGGL((rm_render_direct<SC, true, K, OUT>), grid, block, 0, s, F, out, evals);
-    else hipLaunchKernelGGL((rm_render_direct<SC, false, K, OUT>), grid, block, 0, s, F, out, evals);
+    FrameConst G = F;
+    G.gx_magic = div_magic(grid.x, (uint64_t)grid.x * grid.y);
+    if (evals) hipLaunchKernelGGL((rm_render_direct<SC, true, K, OUT>), grid, block, 0, s, G, out, evals);
+    else hipLaunchKernelGGL((rm_render_direct<SC, false, K, OUT>), grid, block, 0, s, G, out, evals);
     return hipGetLastError();
 }
 
@@ -75,8 +77,10 @@ hipError_t launch_persist(const FrameConst& F, OUT* out, unsigned long long* eva
                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rm_render_persist<SC, false, OUT>, 64, 0);
     if (e != hipSuccess) return e;
     const int waves = std::max(1, std::min(ntiles, cus * std::max(per_cu, 1)));
-    if (evals) hipLaunchKernelGGL((rm_render_persist<SC, true, OUT>), dim3(waves), dim3(64), 0, s, F, out, evals, g.x, ntiles);
-    else hipLaunchKernelGGL((rm_render_persist<SC, false, OUT>), dim3(waves), dim3(64), 0, s, F, out, evals, g.x, ntiles);
+    FrameConst G = F;
+    G.gx_magic = div_magic(g.x, (uint64_t)ntiles);
+    if (evals) hipLaunchKernelGGL((rm_render_persist<SC, true, OUT>), dim3(waves), dim3(64), 0, s, G, out, evals, g.x, ntiles);
+    else hipLaunchKernelGGL((rm_render_persist<SC, false, OUT>), dim3(waves), dim3(64), 0, s, G, out, evals, g.x, ntiles);
     return hipGetLastError();
 }
 

@@ -315,6 +315,7 @@ hipError_t launch_render(const Module& m, const rm::FrameConst& F, void* out, bo
                          hipStream_t s) {
     if (!m.render || !m.render_count) return hipErrorInvalidDeviceFunction;
     rm::FrameConst f = F;
+    f.gx_magic = rm::div_magic((uint32_t)((F.W + 7) / 8), (uint64_t)((F.W + 7) / 8) * (uint64_t)((F.nrows + 7) / 8));
     void* o = out;
     int r8 = rgba8 ? 1 : 0;
     unsigned long long* e = evals;

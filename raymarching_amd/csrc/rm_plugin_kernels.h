@@ -35,8 +35,8 @@ __device__ __forceinline__ void plugin_render_tile(const FrameConst& F, void* ou
     int bx = blockIdx.x, by = blockIdx.y;
     if (F.tile_order) {  // costliest tiles first (rm_params.schedule, rm_set_tile_order)
         const uint32_t t = F.tile_order[by * gridDim.x + bx];
-        bx = t % gridDim.x;
-        by = t / gridDim.x;
+        by = div_by((int)t, F.gx_magic, (int)gridDim.x);
+        bx = (int)t - by * (int)gridDim.x;
     }
     const int x = bx * 8 + (lane & 7), j = by * 8 + (lane >> 3);
     Tally cnt;

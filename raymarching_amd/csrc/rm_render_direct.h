@@ -493,9 +493,25 @@ __device__ __forceinline__ V3 fma3(V3 a, float s, V3 b) {  // a s + b, one round
 }
 __device__ __forceinline__ float dot_fma(V3 a, V3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 
+// RM_AO_LINRAY_T: scene T's four AO probes step along the normal's
+// sponge-space image (q0 + (R n) 0.2 (i + 1), one FMA per axis) instead of
+// transforming each probe point (the AO factor is smooth in the roundings;
+// step counts do not depend on it)
+#ifndef RM_AO_LINRAY_T
+#define RM_AO_LINRAY_T 1
+#endif
 template <int SC, int NB = 3>
 __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tally& cnt, bool plane = false) {
     float sum = 0.0f;
+    if constexpr (SC == SCENE_T && RM_AO_LINRAY_T) {
+        const LinRay r = sponge_ray(F, pos, n);
+#pragma unroll
+        for (int i = 0; i < 4; i++) sum += (1.0f / (float)(1 << i)) * menger_at<NB>(r, (float)(i + 1) * 0.2f, cnt);
+        float maxSum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; i++) maxSum += (1.0f / (float)(1 << i)) * (float)(i + 1) * 0.2f;
+        return sum / maxSum;
+    }
     auto probe = [&](int i) {
         V3 p = kProbeFma<SC> ? fma3(n, (float)(i + 1) * 0.2f, pos) : pos + (n * (float)(i + 1)) * 0.2f;
         sum += (1.0f / (float)(1 << i)) * dist_at<SC, false, NB>(F, p, cnt, plane);
@@ -761,7 +777,7 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
     shading = shading + v3s(fre * occ);
-    return apply_scattering(v3s(c) * shading, ro, p);
+    return apply_scattering<true>(v3s(c) * shading, ro, p);
 }
 
 // BASELINE config-1 scene S0: castRayD + normal + lambert
@@ -835,7 +851,7 @@ __device__ __forceinline__ void store_pixel(const FrameConst& F, OUT* __restrict
 
 // local packed row j of this shard -> frame row y
 __device__ __forceinline__ int shard_row(const FrameConst& F, int j) {
-    int c = j / F.run, r = j - c * F.run;
+    int c = div_by(j, F.run_magic, F.run), r = j - c * F.run;
     return c * F.cycle + F.offset + r;
 }
 
@@ -911,8 +927,8 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
     const bool lat = T::WPB == 1 && SC == SCENE_T && F.tile_order && by * gx + bx < F.lat_tiles;
     if (F.tile_order) {  // dispatch order != tile order (costliest tiles first, rm_set_tile_order)
         const uint32_t t = F.tile_order[by * gx + bx];
-        bx = t % gx;
-        by = t / gx;
+        by = div_by((int)t, F.gx_magic, gx);
+        bx = (int)t - by * gx;
     }
     const int x = bx * T::TW + (w & 1) * 8 + (lane % T::LW);
     const int j = by * T::TH + (w >> 1) * 8 + (lane / T::LW);
@@ -984,7 +1000,8 @@ __device__ __forceinline__ void render_persistent(const FrameConst& F, OUT* __re
     for (int j = ticket(); j < nj;) {
         const int jn = ticket();
         const int k = xcd + 8 * j;
-        render_tile_at<SC, COUNT, KERNEL_PERSIST, OUT>(F, out, evals, k % gx, k / gx, gx);
+        const int ky = div_by((int)k, F.gx_magic, gx);
+        render_tile_at<SC, COUNT, KERNEL_PERSIST, OUT>(F, out, evals, (int)k - ky * gx, ky, gx);
         j = jn;
     }
     if (threadIdx.x == 0) {

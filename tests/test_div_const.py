@@ -46,3 +46,49 @@ def test_div_const_is_correctly_rounded():
             pytest.skip(f"no host C compiler: {e}")
         out = subprocess.run([exe], check=True, capture_output=True, text=True, timeout=120).stdout
         assert int(out.strip()) == 0
+
+
+# rm_device.h div_magic / div_by: the launch's row and tile divisions as one
+# 32-bit high multiply.  Compiled from the header's own host-callable
+# div_magic (a HIP header: hipcc host compile), checked against integer
+# division for every divisor up to 4096 at its largest allowed dividend range
+# (the bound div_magic accepts), on the range's last 2^16 dividends and a
+# stride through the rest.
+MAGIC_SRC = r'''
+#include <stdint.h>
+#include <stdio.h>
+#include "rm_device.h"
+int main(void) {
+    long bad = 0, checked = 0, used = 0;
+    for (uint32_t d = 1; d <= 4096; d++) {
+        // the largest a_end div_magic accepts for d
+        uint64_t lo = 1, hi = (1ull << 32);
+        while (lo < hi) { uint64_t mid = (lo + hi + 1) / 2; if (rm::div_magic(d, mid)) lo = mid; else hi = mid - 1; }
+        const uint32_t m = rm::div_magic(d, lo);
+        if (!m) { if (d >= 2) bad++; continue; }
+        used++;
+        for (uint64_t a = 0; a < lo; a += (a + 65536 < lo ? 977 : 1)) {
+            const uint32_t q = (uint32_t)(((uint64_t)a * m) >> 32);
+            checked++;
+            if (q != (uint32_t)(a / d)) bad++;
+        }
+    }
+    printf("%ld %ld %ld\n", bad, checked, used);
+    return 0;
+}
+'''
+
+
+def test_div_magic_is_floor_division():
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raymarching_amd", "csrc")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "m.cpp"), os.path.join(d, "m")
+        open(src, "w").write(MAGIC_SRC)
+        subprocess.run([hipcc, "-O2", "-x", "hip", "--offload-arch=gfx950", "-I", inc, src, "-o", exe], check=True,
+                       capture_output=True, timeout=300)
+        bad, checked, used = map(int, subprocess.run([exe], check=True, capture_output=True, text=True,
+                                                     timeout=600).stdout.split())
+    assert used == 4095 and checked > 10_000_000 and bad == 0, (bad, checked, used)
