@@ -24,7 +24,7 @@ find $O/trace_C3 -name "*kernel_stats.csv" -exec cp {} $O/bench_C3_kernel_stats.
 timeout -k 10 300 python bench.py --scene O --size 8192 --max-steps 512 --steps 5 --warmup 2 --cpu-seconds 0 > $O/bench_C5frame.json 2> $O/bench_C5frame.err || { echo "bench C5 failed"; tail -20 $O/bench_C5frame.err; exit 6; }
 python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C5 ms/step', round(d['ms_per_step'],4), 'kernel', round(d['kernel_ms'],4), 'frac', d['roofline']['frac'])" $O/bench_C5frame.json
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --backend gloo --cpu-seconds 0 > $O/bench_n2_gloo.json 2> $O/bench_n2_gloo.err || { echo "gloo N=2 failed"; tail -20 $O/bench_n2_gloo.err; exit 7; }
-python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print('N2 gloo ms/step', round(d['ms_per_step'],4), 'frac', r['frac'], 'per_rank', r.get('per_rank_frac'), 'runs', d['balance']['runs'])" $O/bench_n2_gloo.json
+python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); r=d['roofline']; print('N2 gloo ms/step', round(d['ms_per_step'],4), 'frac', r['frac'], 'per_rank', r.get('per_rank_frac'), 'runs', d['balance']['runs'])" $O/bench_n2_gloo.json
 if [ "${PMC:-0}" = 1 ]; then
   bash tools/pmc_profile.sh T4096$TAG || exit 8
   bash tools/pmc_profile.sh O8192$TAG --scene O --size 8192 --max-steps 512 || exit 9
