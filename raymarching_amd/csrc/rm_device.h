@@ -637,7 +637,13 @@ __device__ __forceinline__ V3 apply_scattering(V3 color, V3 ro, V3 p) {
     return color * (1.0f - e) + v3(0.34f, 0.435f, 0.57f) * e;
 }
 // output_shader.frag:178-182
-__device__ __forceinline__ V3 background(V3 ro, V3 rd) { return apply_scattering(v3s(0.0f), ro, ro + rd * ZFAR); }
+// (the sky's fog in the colour-only fast form with RM_FAST_COLOUR, rm_render_direct.h)
+#ifndef RM_FAST_COLOUR
+#define RM_FAST_COLOUR 1
+#endif
+__device__ __forceinline__ V3 background(V3 ro, V3 rd) {
+    return apply_scattering<RM_FAST_COLOUR != 0>(v3s(0.0f), ro, ro + rd * ZFAR);
+}
 
 // RGBA8 unorm of the reference's RenderTexture: clamp, round to nearest
 // (NaN -> 0), R in the low byte

@@ -45,12 +45,12 @@ __device__ __forceinline__ void plugin_render_tile(const FrameConst& F, void* ou
         float tcx, tcy;
         V3 ro, rd;
         camera_ray<false>(F, x, y, tcx, tcy, ro, rd);
-        const float vig = vignette<false>(tcx, tcy);
+        const float vig = vignette<FastColour<SCENE_PLUGIN>::value>(tcx, tcy);
         // the exact skips of scene O's pipeline that hold for any scene (the soft
         // shadows of points facing away from the light): taken
         // by the timed launches, counted by the instrumented ones
         V3 c = render_pixel<SCENE_PLUGIN, 3, COUNT ? 2 : 1>(F, ro, rd, cnt);
-        c = post_colour<false>(c, vig);
+        c = post_colour<FastColour<SCENE_PLUGIN>::value>(c, vig);
         const size_t i = (size_t)j * F.W + x;
         if (rgba8) store_pixel(F, static_cast<uint32_t*>(out), i, c);
         else store_pixel(F, static_cast<float4*>(out), i, c);

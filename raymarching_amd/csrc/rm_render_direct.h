@@ -32,6 +32,29 @@ __device__ __forceinline__ float mpow(float x, float y) {
     if constexpr (FastMath<SC>::value) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
     else return powf(x, y);
 }
+// Colour-only arithmetic (Phong's normalizations and pow, the shadow factor's
+// pow, the SSS term's pow, fog, tonemap, vignette): RM_FAST_COLOUR gives scenes
+// O/OG and plugins the hardware exp2/log2/rsq/rcp forms there too (1-2 ulp).
+// Nothing that positions a ray or feeds the thickness hash changes (marches,
+// normals, the light direction and distance, the floor pattern keep their
+// exact forms), so ray-step counts are untouched and pixels move by ~1e-6.
+#ifndef RM_FAST_COLOUR
+#define RM_FAST_COLOUR 1
+#endif
+template <int SC>
+struct FastColour {
+    static constexpr bool value = FastMath<SC>::value || RM_FAST_COLOUR;
+};
+template <int SC>
+__device__ __forceinline__ float cpow(float x, float y) {
+    if constexpr (FastColour<SC>::value) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+    else return powf(x, y);
+}
+template <int SC>
+__device__ __forceinline__ V3 cnormalize(V3 a) {
+    if constexpr (FastColour<SC>::value) return a * __builtin_amdgcn_rsqf(dot(a, a));
+    else return normalize(a);
+}
 // the scene distance for marches and normals (exact for scene O), and for
 // the AO / shadow / thickness probes, whose results are smooth in the distance
 template <int SC, int NB = 3>
@@ -534,13 +557,13 @@ __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tall
 // the caller's light direction, the same value)
 template <int SC>
 __device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 L, V3 p, V3 eye, V3 N) {
-    V3 V = mnormalize<SC>(eye - p);
-    V3 R = mnormalize<SC>(reflect(-L, N));
+    V3 V = cnormalize<SC>(eye - p);
+    V3 R = cnormalize<SC>(reflect(-L, N));
     float dotLN = dot(L, N);
     float dotRV = dot(R, V);
     if (dotLN < 0.0f) return v3s(0.0f);
     if (dotRV < 0.0f) return k_d * dotLN;
-    return k_d * dotLN + k_s * mpow<SC>(dotRV, alpha);
+    return k_d * dotLN + k_s * cpow<SC>(dotRV, alpha);
 }
 
 // Soft shadows of points facing away from the light: phong returns 0 when
@@ -573,7 +596,7 @@ __device__ __forceinline__ float shadow_if_lit(float dotLN, Tally& cnt, March ma
 
 template <int SC>
 __device__ __forceinline__ V3 shadow_pow(float sha) {
-    if constexpr (FastMath<SC>::value) {  // pow(x, 1) = x; one log2 shared by the other two
+    if constexpr (FastColour<SC>::value) {  // pow(x, 1) = x; one log2 shared by the other two
         const float l = __builtin_amdgcn_logf(sha);
         return v3(sha, __builtin_amdgcn_exp2f(1.2f * l), __builtin_amdgcn_exp2f(1.5f * l));
     }
@@ -646,16 +669,16 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, 
 #endif
     mat = scene_mat<SC>(F, mq);
     float sky = clamp01(0.5f + 0.5f * n.y);
-    float ind = clamp01(dot(n, normalize(lightDir * v3(-1.0f, 0.0f, -1.0f))));
+    float ind = clamp01(dot(n, cnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     V3 shading =
         phong<SC>(v3(1.64f, 1.27f, 0.99f), mat.specular, mat.shininess, lightDir, p, ro, phongN) * shadow_pow<SC>(sha);
     shading = shading + v3(0.16f, 0.20f, 0.28f) * sky * occ;
     shading = shading + v3(0.40f, 0.28f, 0.20f) * ind * occ;
     V3 sssl = lightDir + n * 0.6f;
-    float sssdot = powf(clamp01(dot(-rd, -sssl)), 1.1f) * 0.3f;
+    float sssdot = cpow<SC>(clamp01(dot(-rd, -sssl)), 1.1f) * 0.3f;
     shading = shading + v3s((sssdot + 0.3f) * th);
     V3 color = mat.diffuse * shading + mat.emission;
-    return apply_scattering(color, ro, p);
+    return apply_scattering<FastColour<SC>::value>(color, ro, p);
 }
 
 // output_shader.frag:218-230
@@ -710,6 +733,12 @@ __device__ __forceinline__ V3 render_refraction(const FrameConst& F, V3 ro, V3 r
         rd = tif ? ref : raf;
         ro = p + rd * (0.01f / fabsf(dot(rd, n)));
         invert = tif ? invert : -invert;
+    }
+    if constexpr (FastColour<SC>::value) {
+        constexpr float kLog2e = 1.4426950408889634f;
+        return color * v3(__builtin_amdgcn_exp2f(-absorption.x * absorb * kLog2e),
+                          __builtin_amdgcn_exp2f(-absorption.y * absorb * kLog2e),
+                          __builtin_amdgcn_exp2f(-absorption.z * absorb * kLog2e));
     }
     return color * v3(expf(-absorption.x * absorb), expf(-absorption.y * absorb), expf(-absorption.z * absorb));
 }
@@ -938,7 +967,7 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
         float tcx, tcy;
         V3 ro, rd;
         camera_ray<FastMath<SC>::value>(F, x, y, tcx, tcy, ro, rd);
-        const float vig = vignette<FastMath<SC>::value>(tcx, tcy);
+        const float vig = vignette<FastColour<SC>::value>(tcx, tcy);
         V3 c;
         if constexpr (SC == SCENE_T) {
             // (no settle exit in the latency tiles: their long grazing shadow marches
@@ -950,7 +979,7 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
             (void)lat;
             c = render_pixel<SC, 3, kPlaneSpans<SC> ? (COUNT ? 2 : 1) : 0>(F, ro, rd, cnt);
         }
-        c = post_colour<FastMath<SC>::value>(c, vig);
+        c = post_colour<FastColour<SC>::value>(c, vig);
         store_pixel(F, out, (size_t)j * F.W + x, c);
     }
     if (T::WPB == 1 && F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
