@@ -546,10 +546,24 @@ __device__ __forceinline__ Mat mat_mirror() {  // output_shader.frag:15
     return mat_make(v3s(0.1f), v3s(0.09f), 64.0f, 0.25f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
 }
 // output_shader.frag:16-28
+// (colour only: with RM_FAST_COLOUR the blur width and the divisions by it in
+// the hardware forms; smoothstep is 150-Lipschitz here, so 1-ulp changes of its
+// argument move the colour by ~1e-5 at most)
+#ifndef RM_FAST_COLOUR
+#define RM_FAST_COLOUR 1
+#endif
 __device__ __forceinline__ Mat floor_mat(V3 pos) {
+#if RM_FAST_COLOUR
+    const float l2 = dot(pos, pos);
+    const float scale = fmaxf(10.0f, __builtin_amdgcn_exp2f(0.65f * __builtin_amdgcn_logf(l2)));  // |pos|^1.3
+    const float is = __builtin_amdgcn_rcpf(scale);
+    float tx = smoothstep(-0.005f, 0.005f, glsl_sin(pos.x * PI_REF) * is);
+    float ty = smoothstep(-0.005f, 0.005f, glsl_sin(pos.z * PI_REF) * is);
+#else
     float scale = fmaxf(10.0f, powf(length(pos), 1.3f));
     float tx = smoothstep(-0.005f, 0.005f, glsl_sin(pos.x * PI_REF) / scale);
     float ty = smoothstep(-0.005f, 0.005f, glsl_sin(pos.z * PI_REF) / scale);
+#endif
     float tile = fminf(fmaxf(tx, ty), fmaxf(1.0f - tx, 1.0f - ty));
     V3 color = mix3(v3s(0.3f), v3s(0.025f), tile);
     return mat_make(color, v3s(0.03f), 128.0f, 0.0f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
@@ -638,9 +652,6 @@ __device__ __forceinline__ V3 apply_scattering(V3 color, V3 ro, V3 p) {
 }
 // output_shader.frag:178-182
 // (the sky's fog in the colour-only fast form with RM_FAST_COLOUR, rm_render_direct.h)
-#ifndef RM_FAST_COLOUR
-#define RM_FAST_COLOUR 1
-#endif
 __device__ __forceinline__ V3 background(V3 ro, V3 rd) {
     return apply_scattering<RM_FAST_COLOUR != 0>(v3s(0.0f), ro, ro + rd * ZFAR);
 }

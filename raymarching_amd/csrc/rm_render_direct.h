@@ -38,9 +38,6 @@ __device__ __forceinline__ float mpow(float x, float y) {
 // Nothing that positions a ray or feeds the thickness hash changes (marches,
 // normals, the light direction and distance, the floor pattern keep their
 // exact forms), so ray-step counts are untouched and pixels move by ~1e-6.
-#ifndef RM_FAST_COLOUR
-#define RM_FAST_COLOUR 1
-#endif
 template <int SC>
 struct FastColour {
     static constexpr bool value = FastMath<SC>::value || RM_FAST_COLOUR;
@@ -683,7 +680,7 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, 
 
 // output_shader.frag:218-230
 __device__ __forceinline__ float fresnel(float n2, V3 normal, V3 incident, float reflectivity) {
-    float r0 = (1.0f - n2) / (1.0f + n2);
+    float r0 = RM_FAST_COLOUR ? (1.0f - n2) * __builtin_amdgcn_rcpf(1.0f + n2) : (1.0f - n2) / (1.0f + n2);
     r0 *= r0;
     float x = 1.0f + dot(normal, incident);
     float r = r0 + (1.0f - r0) * x * x * x * x * x;
