@@ -505,7 +505,8 @@ __device__ __forceinline__ float scene_dist(const FrameConst& F, V3 p, Tally& n)
     } else if constexpr (SC == SCENE_PLUGIN) {
         n.evals++;
         n.flop += PluginScene<SC>::flop;
-        return PluginScene<SC>::dist(p);
+        if constexpr (EXACT) return PluginScene<SC>::dist(p);
+        else return PluginScene<SC>::dist_probe(p);
     } else {  // output_shader.frag:38-48
         n.flop += FL_TRANSFORM;
         return scene_dist_O<EXACT>(p, sponge_space<EXACT>(F, p), n);

@@ -192,18 +192,27 @@ std::string translation_unit(const std::string& src, const std::string& file) {
         if (c == '"' || c == '\\') name += '\\';
         name += c;
     }
-    return "#include \"rm_plugin.h\"\n"
-           "namespace rm {\nnamespace glsl {\nnamespace {\n"
-           "#pragma clang force_cuda_host_device begin\n"
-           // (every scene function inlined into the kernels: the uniforms are
-           // read from the kernel-argument segment, rm_plugin.h; GLSL has no
-           // recursion)
-           "#pragma clang attribute push (__attribute__((always_inline)), apply_to = function)\n"
-           "#line 1 \"" + name + "\"\n" +
-           glsl_source(src) +
-           "\n#pragma clang attribute pop\n"
-           "#pragma clang force_cuda_host_device end\n"
-           "}  // namespace\n}  // namespace glsl\n}  // namespace rm\n"
+    // the scene twice: against the library's GLSL-rounding instance (rm::glsl:
+    // marches, normals, rm_scene_eval) and against its probe instance
+    // (rm::glsl::probe, FMA contraction: AO, soft shadows, thickness), as the
+    // built-in scenes have exact and probe forms (rm_sdf_lib_body.h)
+    const std::string scene = glsl_source(src);
+    auto instance = [&](const char* open, const char* close, const char* pre, const char* post) {
+        return std::string(open) + "namespace {\n" + pre +
+               "#pragma clang force_cuda_host_device begin\n"
+               // (every scene function inlined into the kernels: the uniforms are
+               // read from the kernel-argument segment, rm_plugin.h; GLSL has no
+               // recursion)
+               "#pragma clang attribute push (__attribute__((always_inline)), apply_to = function)\n"
+               "#line 1 \"" + name + "\"\n" + scene +
+               "\n#pragma clang attribute pop\n"
+               "#pragma clang force_cuda_host_device end\n" + post + "}  // namespace\n" + close;
+    };
+    return "#include \"rm_plugin.h\"\n" +
+           instance("namespace rm {\nnamespace glsl {\n", "}  // namespace glsl\n}  // namespace rm\n", "", "") +
+           instance("namespace rm {\nnamespace glsl {\nnamespace probe {\n",
+                    "}  // namespace probe\n}  // namespace glsl\n}  // namespace rm\n",
+                    "#pragma clang fp contract(fast)\n", "#pragma clang fp contract(off)\n") +
            "#include \"rm_plugin_kernels.h\"\n";
 }
 

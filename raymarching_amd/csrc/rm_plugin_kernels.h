@@ -12,6 +12,8 @@ struct rm::PluginScene<rm::SCENE_PLUGIN> {
     static constexpr uint32_t flop = 0;
 #endif
     __device__ __forceinline__ static float dist(rm::V3 p) { return rm::glsl::sceneSDF(p).dist; }
+    // the probe form: the scene compiled against the library's probe instance
+    __device__ __forceinline__ static float dist_probe(rm::V3 p) { return rm::glsl::probe::sceneSDF(p).dist; }
     __device__ __forceinline__ static rm::Mat mat(rm::V3 p) { return rm::glsl::sceneSDF(p).mat; }
 };
 
