@@ -97,11 +97,19 @@ __device__ __forceinline__ float smoothstep(float e0, float e1, float x) {
 }
 __device__ __forceinline__ float radians(float d) { return d * 0.017453292519943295f; }
 __device__ __forceinline__ float degrees(float r) { return r * 57.29577951308232f; }
-__device__ __forceinline__ float pow(float x, float y) { return powf(x, y); }
-__device__ __forceinline__ float exp(float x) { return expf(x); }
-__device__ __forceinline__ float exp2(float x) { return exp2f(x); }
-__device__ __forceinline__ float log(float x) { return logf(x); }
-__device__ __forceinline__ float log2(float x) { return log2f(x); }
+// (the probe instance: the hardware exp2 / log2, 1-2 ulp; GLSL allows 3 ulp
+// for exp2/log2 and derives pow from them)
+__device__ __forceinline__ float pow(float x, float y) {
+    return RM_LIB_PROBE ? __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x)) : powf(x, y);
+}
+__device__ __forceinline__ float exp(float x) {
+    return RM_LIB_PROBE ? __builtin_amdgcn_exp2f(x * 1.4426950408889634f) : expf(x);
+}
+__device__ __forceinline__ float exp2(float x) { return RM_LIB_PROBE ? __builtin_amdgcn_exp2f(x) : exp2f(x); }
+__device__ __forceinline__ float log(float x) {
+    return RM_LIB_PROBE ? __builtin_amdgcn_logf(x) * 0.6931471805599453f : logf(x);
+}
+__device__ __forceinline__ float log2(float x) { return RM_LIB_PROBE ? __builtin_amdgcn_logf(x) : log2f(x); }
 __device__ __forceinline__ float sqrt(float x) { return RM_LIB_PROBE ? __builtin_amdgcn_sqrtf(x) : sqrtf(x); }
 __device__ __forceinline__ float inversesqrt(float x) { return 1.0f / sqrtf(x); }
 // sin/cos as the implementation that renders the golden fixtures (rm_device.h glsl_sin)
