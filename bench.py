@@ -302,6 +302,10 @@ def pmc_flop(pmc):
     return slots * (lane_frac or 1.0), slots, lane_frac
 
 
+# a PMC entry counts this build's launch only if its traced duration is within this ratio of the measured one
+PMC_TIME_TOL = (0.9, 1.1)
+
+
 def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=True, rows_frac=1.0):
     """The render kernel's FP32-VALU roofline for one launch of kern_ms that
     executed `executed_steps` ray-steps and wrote out_bytes.
@@ -321,6 +325,14 @@ def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=T
     t = kern_ms / 1e3
     cnt = pmc_flop(pmc) if pmc else None
     base_steps = pmc.get("executed_ray_steps_per_launch") if pmc else None
+    stale = None
+    if exact and pmc and pmc.get("avg_kernel_ns_trace"):
+        # counters of another build: the profiled launch's duration is off this one's by > 10 %
+        ratio = kern_ms * 1e6 / pmc["avg_kernel_ns_trace"]
+        if not PMC_TIME_TOL[0] <= ratio <= PMC_TIME_TOL[1]:
+            stale = (f"the PMC counters in profiles/pmc_counters.json ({pmc.get('source')}) are stale: their launch "
+                     f"took {pmc['avg_kernel_ns_trace'] / 1e6:.4g} ms, this one {kern_ms:.4g} ms")
+            cnt = None
     roof = {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
             "traffic": None, "flop_per_launch": None, "executed_ray_steps_per_launch": executed_steps,
             "ray_steps_per_launch": evals, "kernel_ms": kern_ms}
@@ -343,7 +355,7 @@ def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=T
         if pmc.get("hbm_bytes_per_launch") is not None:
             roof["traffic"] = pmc["hbm_bytes_per_launch"] * (1.0 if exact else rows_frac)
     else:
-        roof["frac_null_reason"] = (
+        roof["frac_null_reason"] = stale or (
             "no PMC counters for this workload in profiles/pmc_counters.json" if cnt is None else
             "the PMC entry of this workload has no executed_ray_steps_per_launch to price a share of it")
     roof["tally_flop_per_launch"] = flop_tally
@@ -360,7 +372,7 @@ def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=T
                            counter_note="rocprofv3 (2 FETCH_SIZE + WRITE_SIZE) per launch"
                                         + ("" if exact else " of the N = 1 frame x this launch's row fraction")
                                         + " / kernel_ms")
-    if exact and pmc and "SQ_INSTS_VALU" in pmc:
+    if exact and pmc and "SQ_INSTS_VALU" in pmc and not stale:
         # issue fractions at the clock the PMC run measured (GRBM_GUI_ACTIVE / 8 XCDs / kernel time):
         # one wave64 VALU instruction per 2 cycles per SIMD (1024 SIMDs), one SALU per cycle per CU (256)
         clk = pmc.get("clock_hz") or 2.4e9
