@@ -224,20 +224,19 @@ def time_fxaa(r, frame8, stream, reps=20):
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": nbytes}
 
 
-# per tap and level: g a, g b, g a b and 12 multiply-adds (the cell polynomial
-# accumulated, rm_post.hip cell_acc); per pixel: 25 taps x 2 levels, the 20
-# bilinear axes (3 each) and 10 tap offsets (2), the base-level fetch (27), the
-# level blend (9), threshold and add (9)
-BLOOM_FLOP_PER_TAP = 2 * (3 + 2 * 12)
-BLOOM_FLOP_PER_PX = 25 * BLOOM_FLOP_PER_TAP + 20 * 3 + 10 * 2 + 27 + 9 + 9
+# per pixel (rm_post.hip rm_bloom_min_kernel): the base-level bilinear fetch
+# (27), per level and channel the run pair's bilinear polynomial (3 multiply-adds,
+# 2 levels x 3 channels), the level sum (3), threshold and add (9).  The run-pair
+# polynomials (25 taps each, double) are per frame, ~1e-3 of this at 4096^2.
+BLOOM_FLOP_PER_PX = 27 + 2 * 3 * 3 * 2 + 3 + 9
 
 
 def time_bloom(r, frame8, stream, reps=20):
     """The reference's bloom pass (bloom.frag + its mip chain, main.cpp:212-214)
-    over the RGBA8 frame on rank 0.  Its roofline is FP32 VALU: per pixel 25
-    taps x 2 levels of the filter-cell polynomial (BLOOM_FLOP_PER_PX), the
-    cells wave-uniform scalar loads.  HBM bytes (frame read twice, written
-    once, mip levels 1..d2 written and read once) are reported beside it."""
+    over the RGBA8 frame on rank 0.  Its roofline is HBM: the frame read twice
+    (mip level 1, the base-level fetch) and written once, mip levels 1..d2
+    written and read once (algorithmic bytes); per pixel two bilinear
+    polynomials (BLOOM_FLOP_PER_PX) are reported beside it."""
     import math
 
     import torch
@@ -258,12 +257,11 @@ def time_bloom(r, frame8, stream, reps=20):
     nbytes = 4 * (3 * W * H + 2 * mip_texels)
     gbs = nbytes / (ms / 1e3) / 1e9
     tflops = W * H * BLOOM_FLOP_PER_PX / (ms / 1e3) / 1e12
-    return {"name": "bloom (shaders/post/bloom.frag:14-43 + mip chain)", "ms": ms, "bound": "valu",
-            "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": tflops / PEAK_FP32_TFLOPS,
-            "flop_per_px": BLOOM_FLOP_PER_PX,
-            "hbm": {"achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-                    "algorithmic_bytes": nbytes},
-            "mip_levels": d2, "texel_fetches_per_px": 4 * (1 + 25 * 2)}
+    return {"name": "bloom (shaders/post/bloom.frag:14-43 + mip chain)", "ms": ms, "bound": "hbm",
+            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+            "algorithmic_bytes": nbytes, "mip_levels": d2,
+            "valu": {"flop_per_px": BLOOM_FLOP_PER_PX, "achieved": tflops, "peak": PEAK_FP32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": tflops / PEAK_FP32_TFLOPS}}
 
 
 def balanced_runs(world, band, H, ex):

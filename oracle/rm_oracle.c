@@ -1207,31 +1207,98 @@ static vec3 tex_bilinear(const uint32_t *img, int w, int h, float u, float v) {
     return v3(o[0], o[1], o[2]);
 }
 
-/* One minified tap of a level accumulated into acc (the HIP path's order,
- * rm_post.hip cell_acc): acc += g (c00 + a Px + b Py + a b Pxy) as
- * acc += c00 g, Px (g a), Py (g b), Pxy (g a b), four fmaf per channel. */
-static vec3 bloom_tap_acc(const uint32_t *img, int w, int h, float u, float v, float g, vec3 acc) {
-    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
-    float fx = floorf(x), fy = floorf(y);
-    float a = x - fx, b = y - fy;
-    int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
-    x0 = x0 < 0 ? 0 : (x0 >= w ? w - 1 : x0);
-    x1 = x1 < 0 ? 0 : (x1 >= w ? w - 1 : x1);
-    y0 = y0 < 0 ? 0 : (y0 >= h ? h - 1 : y0);
-    y1 = y1 < 0 ? 0 : (y1 >= h ? h - 1 : y1);
-    const uint32_t t00 = img[(size_t)y0 * w + x0], t01 = img[(size_t)y0 * w + x1];
-    const uint32_t t10 = img[(size_t)y1 * w + x0], t11 = img[(size_t)y1 * w + x1];
-    const float ga = g * a, gb = g * b, gab = ga * b;
-    float o[3] = {acc.x, acc.y, acc.z};
-    for (int c = 0; c < 3; c++) {
-        const int s = 8 * c;
-        float c00 = (float)((t00 >> s) & 255u) * UNORM_K, c01 = (float)((t01 >> s) & 255u) * UNORM_K;
-        float c10 = (float)((t10 >> s) & 255u) * UNORM_K, c11 = (float)((t11 >> s) & 255u) * UNORM_K;
-        const float px = c01 - c00, py = c10 - c00, pxy = (c11 - c10) - px;
-        o[c] = fmaf(pxy, gab, fmaf(py, gb, fmaf(px, ga, fmaf(c00, g, o[c]))));
-    }
-    return v3(o[0], o[1], o[2]);
+/* bloom.frag:33-43 for lod > 0 as the HIP path sums it (rm_post.hip, "bloom.frag:33-43
+ * for lod > 0"): with the 25 taps' bilinear cells fixed, the weighted 5 x 5 sum of a level
+ * is one bilinear polynomial P00 + P10 s' + P01 t' + P11 s' t' of the pixel's texel-space
+ * position (s' = s - cx_2, t' = t - cy_2).  The pixel columns (rows) fall into runs of equal
+ * cell tuples; each (column run, row run) pair's polynomial is summed in double with the
+ * level's blend weight folded in, then rounded to float.  The same function of the same
+ * texels as the per-tap sum, rounded differently (~1e-6); tests/test_bloom.py pins it to
+ * SwiftShader.  An axis: n pixels of an N-pixel image over a level of lw texels. */
+typedef struct {
+    int n, N, lw, is_y;
+    float off[5]; /* bloom.frag's offset of tap i: u (i iaspect) scale, v j scale */
+} bloom_axis;
+
+static float bloom_coord(const bloom_axis *A, int c) {
+    const float t = ((float)c + 0.5f) / (float)A->N;
+    return (A->is_y ? 1.0f - t : t) * (float)A->lw - 0.5f;
 }
+
+static int bloom_cell(const bloom_axis *A, float coord, int i) {
+    const double d = (double)A->off[i] * (double)A->lw;
+    const double x = floor((double)coord + d);
+    return x < -1.0 ? -1 : (x > (double)(A->lw - 1) ? A->lw - 1 : (int)x);
+}
+
+/* per pixel (sub[c], run[c]); per run its five cells; returns the number of runs */
+static int bloom_runs(const bloom_axis *A, float *sub, int *run, int *tup) {
+    int prev = -1, r = -1;
+    for (int c = 0; c < A->n; c++) {
+        const float coord = bloom_coord(A, c);
+        int cell[5], k = 0;
+        for (int i = 0; i < 5; i++) {
+            cell[i] = bloom_cell(A, coord, i);
+            k += cell[i] + 1;
+        }
+        if (k != prev) {
+            r++;
+            for (int i = 0; i < 5; i++) tup[r * 5 + i] = cell[i];
+        }
+        prev = k;
+        sub[c] = coord - (float)cell[2];
+        run[c] = r;
+    }
+    return r + 1;
+}
+
+static const float BLOOM_G[3][3] = {{41.0f / 273.0f, 26.0f / 273.0f, 7.0f / 273.0f},
+                                    {26.0f / 273.0f, 16.0f / 273.0f, 4.0f / 273.0f},
+                                    {7.0f / 273.0f, 4.0f / 273.0f, 1.0f / 273.0f}};
+
+/* the polynomial of one run pair: out[12] = P00 rgb, P10 rgb, P01 rgb, P11 rgb, times lam */
+static void bloom_poly(const uint32_t *L, const bloom_axis *X, const bloom_axis *Y, const int *cx, const int *cy,
+                       double lam, float *out) {
+    const int w = X->lw, h = Y->lw;
+    double e[5], f[5], P[12] = {0};
+    for (int i = 0; i < 5; i++) {
+        e[i] = ((double)cx[2] + (double)X->off[i] * (double)w) - (double)cx[i];
+        f[i] = ((double)cy[2] + (double)Y->off[i] * (double)h) - (double)cy[i];
+    }
+    for (int j = 0; j < 5; j++) { /* tap row j summed alone (in i order), then the rows in j order */
+        double R[12] = {0};
+        const int y0 = cy[j] < 0 ? 0 : (cy[j] > h - 1 ? h - 1 : cy[j]);
+        const int y1 = cy[j] + 1 < 0 ? 0 : (cy[j] + 1 > h - 1 ? h - 1 : cy[j] + 1);
+        for (int i = 0; i < 5; i++) {
+            const int x0 = cx[i] < 0 ? 0 : (cx[i] > w - 1 ? w - 1 : cx[i]);
+            const int x1 = cx[i] + 1 < 0 ? 0 : (cx[i] + 1 > w - 1 ? w - 1 : cx[i] + 1);
+            const uint32_t t00 = L[(size_t)y0 * w + x0], t01 = L[(size_t)y0 * w + x1];
+            const uint32_t t10 = L[(size_t)y1 * w + x0], t11 = L[(size_t)y1 * w + x1];
+            const double g = (double)BLOOM_G[abs(i - 2)][abs(j - 2)];
+            for (int c = 0; c < 3; c++) {
+                const int s = 8 * c;
+                /* texel units (0..255): 1/255 goes with the blend weight */
+                const double c00 = (double)((t00 >> s) & 255u), c01 = (double)((t01 >> s) & 255u);
+                const double c10 = (double)((t10 >> s) & 255u), c11 = (double)((t11 >> s) & 255u);
+                const double px = c01 - c00, py = c10 - c00, pxy = (c11 - c10) - px;
+                R[c] += g * (((c00 + e[i] * px) + f[j] * py) + (e[i] * f[j]) * pxy);
+                R[3 + c] += g * (px + f[j] * pxy);
+                R[6 + c] += g * (py + e[i] * pxy);
+                R[9 + c] += g * pxy;
+            }
+        }
+        for (int q = 0; q < 12; q++) P[q] += R[q];
+    }
+    const double scale = lam * (1.0 / 255.0);
+    for (int q = 0; q < 12; q++) out[q] = (float)(P[q] * scale);
+}
+
+/* the two levels' run tables of one image (lod > 0) */
+typedef struct {
+    float *sub[4];
+    int *run[4], *tup[4], nruns[4];
+    float *tab[2];
+} bloom_runs_t;
 
 /* The levels bloom.frag reads: textureLod at lod = log2(0.05 * u_resolution.y)
  * (bloom.frag:22, u_resolution = the image size, post_bloom.cpp:6) blends
@@ -1253,33 +1320,32 @@ int oracle_bloom_levels(int W, int H, float *lod, int *d1, int *d2) {
     return b + 1;
 }
 
-/* bloom.frag:33-43 at output pixel (x, y); levels[k] is lw[k] x lh[k] */
+/* bloom.frag:33-43 at output pixel (x, y); levels[k] is lw[k] x lh[k]; B = the run
+ * tables when lod > 0 */
 static uint32_t bloom_pixel(const uint32_t *const *levels, const int *lw, const int *lh, int W, int H, int x, int y,
-                            float lod, int d1, int d2) {
-    static const float G[3][3] = {{41.0f / 273.0f, 26.0f / 273.0f, 7.0f / 273.0f},
-                                  {26.0f / 273.0f, 16.0f / 273.0f, 4.0f / 273.0f},
-                                  {7.0f / 273.0f, 4.0f / 273.0f, 1.0f / 273.0f}};
+                            float lod, const bloom_runs_t *B) {
     const float tcx = ((float)x + 0.5f) / (float)W, tcy = ((float)y + 0.5f) / (float)H;
     const float u = tcx, v = 1.0f - tcy; /* bloom.frag:36 */
     vec3 color = tex_bilinear(levels[0], lw[0], lh[0], u, v);
-    const float scale = 0.05f, iaspect = (float)H / (float)W, fr = lod - floorf(lod);
-    vec3 bl = v3(0.0f, 0.0f, 0.0f), b2 = v3(0.0f, 0.0f, 0.0f);
-    for (int j = -2; j <= 2; j++)     /* bloom.frag:24-26 */
-        for (int i = -2; i <= 2; i++) {
-            const float uu = u + ((float)i * iaspect) * scale, vv = v + (float)j * scale;
-            const float g = G[abs(i)][abs(j)];
-            if (lod <= 0.0f) {
+    const float scale = 0.05f, iaspect = (float)H / (float)W;
+    vec3 bl = v3(0.0f, 0.0f, 0.0f);
+    if (lod <= 0.0f) {
+        for (int j = -2; j <= 2; j++) /* bloom.frag:24-26 */
+            for (int i = -2; i <= 2; i++) {
+                const float uu = u + ((float)i * iaspect) * scale, vv = v + (float)j * scale;
+                const float g = BLOOM_G[abs(i)][abs(j)];
                 const vec3 s = tex_bilinear(levels[0], lw[0], lh[0], uu, vv);
                 bl = v3(fmaf(g, s.x, bl.x), fmaf(g, s.y, bl.y), fmaf(g, s.z, bl.z));
-            } else {
-                /* sum g ((1 - fr) s1 + fr s2) = (1 - fr) sum g s1 + fr sum g s2: the
-                 * Gaussian sums of the two levels, blended once at the end */
-                bl = bloom_tap_acc(levels[d1], lw[d1], lh[d1], uu, vv, g, bl);
-                b2 = bloom_tap_acc(levels[d2], lw[d2], lh[d2], uu, vv, g, b2);
             }
+    } else {
+        float val[2][3];
+        for (int l = 0; l < 2; l++) {
+            const float sx = B->sub[2 * l][x], sy = B->sub[2 * l + 1][y];
+            const float *q = B->tab[l] + ((size_t)B->run[2 * l + 1][y] * B->nruns[2 * l] + B->run[2 * l][x]) * 12;
+            for (int c = 0; c < 3; c++) val[l][c] = fmaf(fmaf(q[9 + c], sx, q[6 + c]), sy, fmaf(q[3 + c], sx, q[c]));
         }
-    if (lod > 0.0f)
-        bl = v3((1.0f - fr) * bl.x + fr * b2.x, (1.0f - fr) * bl.y + fr * b2.y, (1.0f - fr) * bl.z + fr * b2.z);
+        bl = v3(val[0][0] + val[1][0], val[0][1] + val[1][1], val[0][2] + val[1][2]);
+    }
     color = v3(color.x + gmax(bl.x - 0.3f, 0.0f), color.y + gmax(bl.y - 0.3f, 0.0f),
                color.z + gmax(bl.z - 0.3f, 0.0f)); /* bloom.frag:28,41 (intensity 1) */
     return unorm8(color.x) | (unorm8(color.y) << 8) | (unorm8(color.z) << 16) | (255u << 24);
@@ -1311,9 +1377,52 @@ int oracle_bloom(int W, int H, const uint32_t *in, uint32_t *out, uint32_t *mips
         levels[k] = buf + off;
         off += (size_t)lw[k] * lh[k];
     }
+    bloom_runs_t B;
+    memset(&B, 0, sizeof(B));
+    int bad = 0;
+    if (lod > 0.0f) {
+        const float fr = lod - floorf(lod), iaspect = (float)H / (float)W, scale = 0.05f;
+        bloom_axis ax[4];
+        for (int a = 0; a < 4; a++) {
+            const int lvl = a < 2 ? d1 : d2;
+            ax[a].is_y = a & 1;
+            ax[a].n = ax[a].N = ax[a].is_y ? H : W;
+            ax[a].lw = ax[a].is_y ? lh[lvl] : lw[lvl];
+            for (int i = 0; i < 5; i++)
+                ax[a].off[i] = ax[a].is_y ? (float)(i - 2) * scale : ((float)(i - 2) * iaspect) * scale;
+            B.sub[a] = (float *)malloc(sizeof(float) * ax[a].n);
+            B.run[a] = (int *)malloc(sizeof(int) * ax[a].n);
+            B.tup[a] = (int *)malloc(sizeof(int) * 5 * (size_t)ax[a].n);
+            if (!B.sub[a] || !B.run[a] || !B.tup[a]) bad = 1;
+            else B.nruns[a] = bloom_runs(&ax[a], B.sub[a], B.run[a], B.tup[a]);
+        }
+        for (int l = 0; l < 2 && !bad; l++) {
+            const int nx = B.nruns[2 * l], ny = B.nruns[2 * l + 1];
+            const double lam = l == 0 ? (double)(1.0f - fr) : (double)fr;
+            B.tab[l] = (float *)malloc(sizeof(float) * 12 * (size_t)nx * ny);
+            if (!B.tab[l]) {
+                bad = 1;
+                break;
+            }
 #pragma omp parallel for schedule(static)
-    for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++) out[(size_t)y * W + x] = bloom_pixel(levels, lw, lh, W, H, x, y, lod, d1, d2);
+            for (int ry = 0; ry < ny; ry++)
+                for (int rx = 0; rx < nx; rx++)
+                    bloom_poly(levels[l == 0 ? d1 : d2], &ax[2 * l], &ax[2 * l + 1], B.tup[2 * l] + rx * 5,
+                               B.tup[2 * l + 1] + ry * 5, lam, B.tab[l] + ((size_t)ry * nx + rx) * 12);
+        }
+    }
+    if (!bad) {
+#pragma omp parallel for schedule(static)
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++) out[(size_t)y * W + x] = bloom_pixel(levels, lw, lh, W, H, x, y, lod, &B);
+    }
+    for (int a = 0; a < 4; a++) {
+        free(B.sub[a]);
+        free(B.run[a]);
+        free(B.tup[a]);
+    }
+    free(B.tab[0]);
+    free(B.tab[1]);
     if (!mips) free(buf);
-    return 0;
+    return bad ? 2 : 0;
 }

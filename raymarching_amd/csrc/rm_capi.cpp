@@ -73,6 +73,8 @@ struct rm_ctx {
     size_t staging_bytes = 0;
     uint32_t *mips = nullptr;  // bloom's mip levels 1..d2
     size_t mips_texels = 0;
+    int bloom_runs_w = 0, bloom_runs_h = 0;  // the size whose bloom run tables `mips` holds (0: none)
+    hipStream_t bloom_runs_stream = nullptr;
     rmplugin::Module plugin;  // the loaded scene plugin (scene == SCENE_PLUGIN)
     uint32_t *tile_order = nullptr;  // rm_set_tile_order (device copy)
     int64_t tile_order_n = 0;
@@ -1191,11 +1193,19 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
         if (ctx->mips) RM_HIP(hipFree(ctx->mips));
         ctx->mips = nullptr;
         ctx->mips_texels = 0;
+        ctx->bloom_runs_w = 0;
         RM_HIP(hipMalloc(&ctx->mips, plan.texels * sizeof(uint32_t)));
         ctx->mips_texels = plan.texels;
     }
-    hipError_t e = rm::launch_bloom(in, out, ctx->mips, plan, ctx->stream);
+    // the run tables depend on W x H only; reused when the last bloom of this
+    // context had the same size and stream (same buffer)
+    const bool cached = ctx->bloom_runs_w == W && ctx->bloom_runs_h == H && ctx->bloom_runs_stream == ctx->stream;
+    ctx->bloom_runs_w = 0;
+    hipError_t e = rm::launch_bloom(in, out, ctx->mips, plan, ctx->stream, cached);
     if (e != hipSuccess) return hip_fail(ctx, e, "bloom launch");
+    ctx->bloom_runs_w = W;
+    ctx->bloom_runs_h = H;
+    ctx->bloom_runs_stream = ctx->stream;
     return mark_done(ctx);
 }
 

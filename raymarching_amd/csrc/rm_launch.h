@@ -76,9 +76,17 @@ struct BloomPlan {
     int d1 = 0, d2 = 0;
     int w[40] = {}, h[40] = {};
     size_t offset[40] = {}, texels = 0;
-    size_t cell_offset = 0;  // lod > 0: the filter cells of levels d1, d2 (words from the buffer start)
+    // lod > 0 (words from the buffer start): the base level's bilinear axes
+    // (per column, per row); per axis (d1 x, d1 y, d2 x, d2 y) the pixels' run
+    // entries, the runs' cell tuples and the run counts; per level the run-pair
+    // polynomials (rm_post.hip).  All but the polynomials depend on W x H only.
+    size_t base_ent[2] = {}, run_ent[4] = {}, run_tup[4] = {}, run_count = 0, poly_tab[2] = {};
+    int nruns[4] = {};  // most runs an axis can have
 };
 BloomPlan bloom_plan(int W, int H);
-hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s);
+// runs_cached: the buffer already holds this W x H's run tables, written on
+// this stream (only the mip levels and the polynomials are rebuilt)
+hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s,
+                        bool runs_cached);
 
 }  // namespace rm

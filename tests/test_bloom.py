@@ -72,6 +72,55 @@ def test_lod_levels(W, H, d1, d2):
     assert (a, b) == (d1, d2)
 
 
+def _per_tap_bloom(img, levels):
+    """bloom.frag for lod > 0 by its definition, in float64: 25 bilinear taps
+    per level (CLAMP_TO_EDGE, texel centres), the two levels blended by fr."""
+    H, W = img.shape
+    lod, d1, d2 = oracle.bloom_levels(W, H)
+    fr = lod - np.floor(lod)
+    G = np.array([[41, 26, 7], [26, 16, 4], [7, 4, 1]]) / 273.0
+    u = (np.arange(W) + 0.5) / W
+    v = 1.0 - (np.arange(H) + 0.5) / H
+    c = channels(img)[..., :3] / 255.0
+
+    def bilinear(L, uu, vv):
+        h, w = L.shape[:2]
+        x = uu * w - 0.5
+        y = vv * h - 0.5
+        fx, fy = np.floor(x), np.floor(y)
+        a, b = (x - fx)[None, :, None], (y - fy)[:, None, None]
+        x0, x1 = np.clip(fx, 0, w - 1).astype(int), np.clip(fx + 1, 0, w - 1).astype(int)
+        y0, y1 = np.clip(fy, 0, h - 1).astype(int), np.clip(fy + 1, 0, h - 1).astype(int)
+        return ((1 - b) * ((1 - a) * L[np.ix_(y0, x0)] + a * L[np.ix_(y0, x1)])
+                + b * ((1 - a) * L[np.ix_(y1, x0)] + a * L[np.ix_(y1, x1)]))
+
+    lv = [channels(m)[..., :3] / 255.0 for m in levels]
+    acc = 0.0
+    for L, wgt in ((lv[d1 - 1], 1 - fr), (lv[d2 - 1], fr)):
+        for j in range(-2, 3):
+            for i in range(-2, 3):
+                acc = acc + wgt * G[abs(i), abs(j)] * bilinear(L, u + i * (H / W) * 0.05, v + j * 0.05)
+    base = bilinear(c, u, v)
+    out = np.clip(base + np.maximum(acc - 0.3, 0.0), 0.0, 1.0)
+    return np.rint(out * 255.0).astype(np.int64)
+
+
+@pytest.mark.parametrize("W,H", [(256, 256), (300, 200), (96, 54), (64, 700)])
+def test_oracle_runs_equal_per_tap_sum(W, H):
+    """The oracle (and the HIP path, bit-exact to it) sums each level's 25 taps
+    as one bilinear polynomial per (column run, row run) pair of cells; that is
+    the per-tap sum of bloom.frag rounded differently: within 1 LSB of a
+    float64 per-tap evaluation over the oracle's own mip levels, and identical
+    on >= 99.5 % of the channels."""
+    rng = np.random.default_rng(W * 31 + H)
+    img = rng.integers(0, 2 ** 32, (H, W), dtype=np.uint64).astype(np.uint32)
+    out, levels = oracle.bloom(img)
+    ref = _per_tap_bloom(img, levels)
+    d = np.abs(channels(out)[..., :3] - ref)
+    assert d.max() <= 1
+    assert np.mean(d == 0) >= 0.995, float(np.mean(d == 0))
+
+
 # ------------------------------------------------------------ GPU
 
 
