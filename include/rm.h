@@ -274,7 +274,9 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
  * the 25-tap trilinear bloom is added to the frame; RGBA8 out, alpha 1.  As in
  * the shader, the output is flipped vertically (uv = (tc.x, 1 - tc.y)).
  * in/out: W x H device buffers, row 0 first, in != out.  Asynchronous on the
- * context's stream. */
+ * context's stream.  The scratch buffer also keeps the size's run tables
+ *  between calls; they are rebuilt when W x H or the context's
+ * stream changes. */
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
 
 /* ---- Weighted row parts: frame row y belongs to a part iff (y mod cycle) - offset
