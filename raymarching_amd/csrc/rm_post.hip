@@ -189,9 +189,11 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     for (int k = 0; k < NR; k++) {
         const int r = wv + 4 * k;
         const int gy = clamp_med3(ty0 + (r < FXL_H ? r : FXL_H - 1), H - 1);
-        const char* row = reinterpret_cast<const char*>(in) + (uint32_t)(gy * W) * 4u;
-        t0[k] = *reinterpret_cast<const uint32_t*>(row + (uint32_t)gx0 * 4u);
-        t1[k] = *reinterpret_cast<const uint32_t*>(row + (uint32_t)gx1 * 4u);
+        // one 32-bit byte offset from the kernel-argument base per load (the
+        // saddr form: no 64-bit address add; frames < 2^30 texels)
+        const uint32_t rowoff = __umul24((uint32_t)gy, (uint32_t)W);  // (W, H <= 2^20: 24-bit operands)
+        t0[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(in) + (rowoff + (uint32_t)gx0) * 4u);
+        t1[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(in) + (rowoff + (uint32_t)gx1) * 4u);
     }
 #pragma unroll
     for (int k = 0; k < NR; k++) {
@@ -270,8 +272,14 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
         const uint32_t tM = stex[m];
 #endif
         const float fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_lane), ly));
-        const float lMin = fminf(lM, fminf(fminf(lNW, lNE), fminf(lSW, lSE)));
-        const float lMax = fmaxf(lM, fmaxf(fmaxf(lNW, lNE), fmaxf(lSW, lSE)));
+        // (lumas are never NaN or -0: IEEE minimum/maximum, v_minimum3/v_maximum3,
+        // equal GLSL min/max here without minNum's canonicalizing v_max per operand)
+        const float lMin = __builtin_elementwise_minimum(
+            lM, __builtin_elementwise_minimum(__builtin_elementwise_minimum(lNW, lNE),
+                                              __builtin_elementwise_minimum(lSW, lSE)));
+        const float lMax = __builtin_elementwise_maximum(
+            lM, __builtin_elementwise_maximum(__builtin_elementwise_maximum(lNW, lNE),
+                                              __builtin_elementwise_maximum(lSW, lSE)));
         float dx = -((lNW + lNE) - (lSW + lSE));
         float dy = ((lNW + lSW) - (lNE + lSE));
         float dirReduce = fmaxf((lNW + lNE + lSW + lSE) * (0.25f * FXAA_REDUCE_MUL), FXAA_REDUCE_MIN);
