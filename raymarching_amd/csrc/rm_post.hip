@@ -144,6 +144,9 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #ifndef RM_FXAA_F4
 #define RM_FXAA_F4 0
 #endif
+#ifndef RM_FXAA_ROWS
+#define RM_FXAA_ROWS 2  // rows per pass of a wave (2 or 4)
+#endif
 constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
 constexpr int FXL_MAX_DIM = 1 << 20;
 static_assert((FXL_TY & (FXL_TY - 1)) == 0 && FXL_TY <= 64, "fy_lane: one lane per tile row");
@@ -311,13 +314,23 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
         // alpha stays the texel's own byte: (b / 255) * 255 rounds back to b)
         return unorm8_finite(c.r) | (unorm8_finite(c.g) << 8) | (unorm8_finite(c.b) << 16) | (tM & 0xff000000u);
     };
-    // two rows at a time: their dependent chains (LDS taps -> division -> span
-    // taps) interleave
+    // RM_FXAA_ROWS rows at a time: their dependent chains (LDS taps -> division
+    // -> span taps) interleave
+#if RM_FXAA_ROWS == 4
+    for (int ly = wv; ly < FXL_TY; ly += 16) {
+        const uint32_t v0 = pixel(ly), v1 = pixel(ly + 4), v2 = pixel(ly + 8), v3 = pixel(ly + 12);
+        if (x < W && y0 + ly < H) out[(size_t)(y0 + ly) * W + x] = v0;
+        if (x < W && y0 + ly + 4 < H) out[(size_t)(y0 + ly + 4) * W + x] = v1;
+        if (x < W && y0 + ly + 8 < H) out[(size_t)(y0 + ly + 8) * W + x] = v2;
+        if (x < W && y0 + ly + 12 < H) out[(size_t)(y0 + ly + 12) * W + x] = v3;
+    }
+#else
     for (int ly = wv; ly < FXL_TY; ly += 8) {
         const uint32_t v0 = pixel(ly), v1 = pixel(ly + 4);
         if (x < W && y0 + ly < H) out[(size_t)(y0 + ly) * W + x] = v0;
         if (x < W && y0 + ly + 4 < H) out[(size_t)(y0 + ly + 4) * W + x] = v1;
     }
+#endif
 }
 
 #ifndef RM_FXAA_LDS
