@@ -773,6 +773,13 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
     constexpr int SC = SCENE_T;
     V3 p = ro + rd * cast_ray_T<NB>(F, sponge_ray(F, ro, rd), cnt);
     V3 n = normal_fast<SC, NB>(F, p, cnt);
+#ifdef RM_DOUBLE_NORMAL  // (analysis: the normal's cost, evaluated twice, same frame)
+    {
+        Tally c2;
+        const V3 n2 = normal_fast<SC, NB>(F, p + v3s(1e-7f), c2);
+        n = n + n2 * 0.0f;
+    }
+#endif
     // getColorReflect (common.frag:991-1002); its dead nr normal is skipped
     V3 rdir = reflect(rd, n);
     V3 ror = p + rdir * 0.01f;
@@ -787,6 +794,12 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
     float ld2 = dot(Ld, Ld);
     V3 lightDir = Ld * __builtin_amdgcn_rsqf(ld2);
     float occ = ao_real<SC, NB>(F, p, n, cnt);
+#ifdef RM_DOUBLE_AO  // (analysis: the AO's cost, evaluated twice, same frame)
+    {
+        Tally c2;
+        occ = occ + ao_real<SC, NB>(F, p + v3s(1e-7f), n, c2) * 0.0f;
+    }
+#endif
 #ifdef RM_ABLATE_SHADOW
     float sha = 1.0f;
 #else
