@@ -146,7 +146,7 @@ def test_hip_bloom_bit_exact_vs_oracle(R, path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("W,H", [(1, 1), (7, 3), (33, 65), (1920, 1080), (4096, 16), (16, 4096), (300, 2000),
-                                 (2048, 1152), (4096, 4096)])
+                                 (2048, 1152), (4096, 2048), (4096, 4096)])  # (pyramid kernels <1>, <2>, <3>)
 def test_hip_bloom_ragged_sizes(R, W, H):
     import torch
     rng = np.random.default_rng(W * 7919 + H)
@@ -154,6 +154,35 @@ def test_hip_bloom_ragged_sizes(R, W, H):
     out = R.bloom(torch.from_numpy(src.astype(np.int32)).cuda()).cpu().numpy().astype(np.uint32)
     ref, _ = oracle.bloom(src)
     assert np.array_equal(out, ref), float(np.mean(out != ref))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H", [(1024, 512), (1000, 600)])  # exact-halving pyramid / per-level mip launches
+def test_hip_bloom_cached_run_tables(R, W, H):
+    """The run tables depend on W x H only and are kept between calls of one
+    size on one stream: a second image of the same size reuses them, a change
+    of size or of the context's stream rebuilds them -- bit-exact every time."""
+    import torch
+    rng = np.random.default_rng(W + 7 * H)
+    imgs = [rng.integers(0, 2 ** 32, (H, W), dtype=np.uint64).astype(np.uint32) for _ in range(2)]
+    small = rng.integers(0, 2 ** 32, (H // 2, W // 2), dtype=np.uint64).astype(np.uint32)
+
+    def run(img):
+        out = R.bloom(torch.from_numpy(img.astype(np.int32)).cuda())
+        torch.cuda.synchronize()
+        return out.cpu().numpy().astype(np.uint32)
+
+    for img in (imgs[0], imgs[1], small, imgs[1]):  # cached, cached, rebuilt (size), rebuilt (size)
+        assert np.array_equal(run(img), oracle.bloom(img)[0])
+    s = torch.cuda.Stream()
+    try:
+        with torch.cuda.stream(s):
+            R.set_stream(s)
+            got = run(imgs[0])  # rebuilt (stream)
+    finally:
+        R.set_stream(torch.cuda.current_stream())
+    assert np.array_equal(got, oracle.bloom(imgs[0])[0])
+    assert np.array_equal(run(imgs[1]), oracle.bloom(imgs[1])[0])
 
 
 @pytest.mark.gpu
