@@ -94,9 +94,9 @@ def _per_tap_bloom(img, levels):
         return ((1 - b) * ((1 - a) * L[np.ix_(y0, x0)] + a * L[np.ix_(y0, x1)])
                 + b * ((1 - a) * L[np.ix_(y1, x0)] + a * L[np.ix_(y1, x1)]))
 
-    lv = [channels(m)[..., :3] / 255.0 for m in levels]
+    lv = [c] + [channels(m)[..., :3] / 255.0 for m in levels]  # lv[k]: level k
     acc = 0.0
-    for L, wgt in ((lv[d1 - 1], 1 - fr), (lv[d2 - 1], fr)):
+    for L, wgt in ((lv[d1], 1 - fr), (lv[d2], fr)):
         for j in range(-2, 3):
             for i in range(-2, 3):
                 acc = acc + wgt * G[abs(i), abs(j)] * bilinear(L, u + i * (H / W) * 0.05, v + j * 0.05)
@@ -105,7 +105,7 @@ def _per_tap_bloom(img, levels):
     return np.rint(out * 255.0).astype(np.int64)
 
 
-@pytest.mark.parametrize("W,H", [(256, 256), (300, 200), (96, 54), (64, 700)])
+@pytest.mark.parametrize("W,H", [(256, 256), (300, 200), (96, 54), (64, 700), (300, 30), (1000, 24)])
 def test_oracle_runs_equal_per_tap_sum(W, H):
     """The oracle (and the HIP path, bit-exact to it) sums each level's 25 taps
     as one bilinear polynomial per (column run, row run) pair of cells; that is
@@ -146,7 +146,8 @@ def test_hip_bloom_bit_exact_vs_oracle(R, path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("W,H", [(1, 1), (7, 3), (33, 65), (1920, 1080), (4096, 16), (16, 4096), (300, 2000),
-                                 (2048, 1152), (4096, 2048), (4096, 4096)])  # (pyramid kernels <1>, <2>, <3>)
+                                 (2048, 1152), (4096, 2048), (4096, 4096),  # (pyramid kernels <1>, <2>, <3>)
+                                 (300, 30), (16384, 24)])  # (0 < lod < 1: level d1 is the frame itself)
 def test_hip_bloom_ragged_sizes(R, W, H):
     import torch
     rng = np.random.default_rng(W * 7919 + H)
