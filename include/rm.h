@@ -91,7 +91,8 @@ typedef struct rm_stats {
     int32_t dispatch; /* RM_DISPATCH_*: the tile order this launch ran (ABI 3)           */
     int32_t lat_tiles; /* scene T: workgroups that rendered with the latency-optimized
                          fold tests (the costliest tiles at the head of an ordered
-                         launch); 0 otherwise (ABI 3)                   */
+                         launch of at most 98304 tiles); 0 otherwise
+                         (ABI 3)                                                        */
     float gather_ms;   /* rm_render_sharded*: device time of the RGB8 pack and the gather
                          on this rank's stream (rank 0: until every wire has arrived,
                          so it includes waiting for the slowest rank); 0 elsewhere (ABI 3) */

@@ -333,6 +333,18 @@ int lat_tiles() {
     }();
     return n;
 }
+// ... in launches short enough for their tail to show: a rank's share, a 1080p
+// frame.  The C4 share at N = 8 (32768 tiles) takes 0.077 ms per pipelined
+// frame with them and 0.098 without; a whole 4096^2 frame (262144 tiles) runs
+// 0.4 % faster without them, an N = 2 half frame (131072) the same either way
+// (profiles/r05/knob_lat_r05.log, lat_share_r05.jsonl): launches of more tiles
+// than this take none (an RM_LAT_TILES setting applies to every launch).
+constexpr int64_t kLatMaxTiles = 98304;
+int lat_tiles_for(int kernel, int W, int nrows) {
+    static const bool forced = std::getenv("RM_LAT_TILES") != nullptr;
+    const rm::TileGrid g = rm::tile_grid(kernel, W, nrows);
+    return forced || (int64_t)g.x * g.y <= kLatMaxTiles ? lat_tiles() : 0;
+}
 
 // Launches per dispatch-order sort of a geometry (rm_ctx::Sched): 16 -- an
 // order is at most 17 launches old (frame-to-frame coherence keeps it good, the
@@ -391,6 +403,8 @@ int rows_of_part(int H, const RowPart &p) {
     return (int)(full * p.run + tail);
 }
 
+int pick_kernel(const rm_ctx *c);
+
 FrameConst frame_const(const rm_ctx *c, int W, int H, const RowPart &part, int nrows) {
     FrameConst F;
     std::memset(&F, 0, sizeof(F));
@@ -416,7 +430,7 @@ FrameConst frame_const(const rm_ctx *c, int W, int H, const RowPart &part, int n
     F.max_steps = c->params.max_steps;
     // 0 (unbounded, the reference) travels as INT_MAX: one compare per shadow step
     F.shadow_max_steps = c->params.shadow_max_steps > 0 ? c->params.shadow_max_steps : 0x7fffffff;
-    F.lat_tiles = lat_tiles();
+    F.lat_tiles = lat_tiles_for(pick_kernel(c), W, nrows);
     for (int i = 0; i < 32; i++) {
         F.hash11[i] = hash11((float)i);
         F.sss_floor[0][i] = sss_floor_term(1.0f, i);
