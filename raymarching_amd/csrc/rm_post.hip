@@ -147,6 +147,9 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #ifndef RM_FXAA_ROWS
 #define RM_FXAA_ROWS 2  // rows per pass of a wave (2 or 4)
 #endif
+#ifndef RM_FXAA_LINEAR
+#define RM_FXAA_LINEAR 0
+#endif
 constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
 constexpr int FXL_MAX_DIM = 1 << 20;
 static_assert((FXL_TY & (FXL_TY - 1)) == 0 && FXL_TY <= 64, "fy_lane: one lane per tile row");
@@ -185,6 +188,32 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     // staging: wave wv loads block rows wv, wv + 4, ...; lane -> column lane and
     // lane + 64 (the last FXL_W - 64 columns); every load in flight before the
     // first LDS store
+#if RM_FXAA_LINEAR && !RM_FXAA_F4
+    // RM_FXAA_LINEAR: the block's texels in row-major order, 256 per pass (13
+    // passes for 74 x 42), so every lane's load and luma is a staged texel
+    // (the column layout above loads 22 words per lane and forms the lumas of
+    // the last ten columns in full-wave instructions for ten lanes)
+    {
+        constexpr int NT = FXL_H * FXL_W, NP = (NT + 255) / 256;
+        uint32_t tt[NP];
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            const int idx = min((int)threadIdx.x + 256 * k, NT - 1);
+            const int r = idx / FXL_W, c = idx - r * FXL_W;  // (constant divisor: a multiply-high)
+            const int gy = clamp_med3(ty0 + r, H - 1), gx = clamp_med3(tx0 + c, W - 1);
+            const uint32_t off = __umul24((uint32_t)gy, (uint32_t)W) + (uint32_t)gx;  // (W, H <= 2^20)
+            tt[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(in) + off * 4u);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            const int idx = (int)threadIdx.x + 256 * k;
+            if (k < NP - 1 || idx < NT) {
+                stex[idx] = tt[k];
+                slum[idx] = luma(rgb(tt[k]));
+            }
+        }
+    }
+#else
     constexpr int NR = (FXL_H + 3) / 4;
     const int gx0 = clamp_med3(tx0 + lane, W - 1), gx1 = clamp_med3(tx0 + 64 + (lane < FXL_W - 64 ? lane : 0), W - 1);
     uint32_t t0[NR], t1[NR];
@@ -221,6 +250,7 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
 #endif
         }
     }
+#endif
     __syncthreads();
     const float FXAA_REDUCE_MIN = 1.0f / 128.0f, FXAA_REDUCE_MUL = 1.0f / 8.0f, FXAA_SPAN_MAX = 8.0f;
     const float ivx = 1.0f / (float)W, ivy = 1.0f / (float)H;  // inverseVP = 1 / u_resolution

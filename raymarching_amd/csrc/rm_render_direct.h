@@ -126,6 +126,11 @@ __device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt,
 // on step exhaustion) and the point whose SdResult is returned.  One exit
 // test per step; at a hit depth is left as it was, so the hit flag and depth
 // give the three outcomes after the loop.
+// RM_O_SPAN_UNIFORM: the floor-plane span test of scene O's march and shadow
+// steps as a wave-uniform branch (see cast_ray_d)
+#ifndef RM_O_SPAN_UNIFORM
+#define RM_O_SPAN_UNIFORM 0
+#endif
 template <int SC, bool INSIDE>
 __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V3& last_q, Tally& cnt) {
     float depth = ZNEAR;
@@ -136,7 +141,14 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
         const float ia = plane_rate(rd);
         float t_plane = 0.0f, last = 0.0f;
         for (int i = 0; i < F.max_steps; i++) {
+#if RM_O_SPAN_UNIFORM
+            // (wave-uniform: a wave with a lane past its span evaluates sceneSDF on every
+            // lane; inside a span that is the plane's value bit for bit, so the lanes'
+            // results are the same, with no exec-mask split per step)
+            if (__builtin_amdgcn_ballot_w64(!(depth < t_plane)) == 0) {
+#else
             if (depth < t_plane) {
+#endif
                 res = ro.y + rd.y * depth;
                 cnt.evals++;
                 cnt.flop += 2;
@@ -271,7 +283,11 @@ __device__ __forceinline__ float soft_shadow2_loop(const FrameConst& F, V3 ro, V
         if constexpr (SM == 2) cnt.skipped += was_settled ? 1u : 0u;
         if constexpr (SC == SCENE_PLUGIN) {
             h = dist_probe<SC>(F, at(w, t), cnt);
+#if RM_O_SPAN_UNIFORM
+        } else if (__builtin_amdgcn_ballot_w64(!(t < t_plane)) == 0) {  // (as cast_ray_d)
+#else
         } else if (t < t_plane) {
+#endif
             h = fmaf(w.d.y, t, w.o.y);  // at(w, t).y
             cnt.evals++;
             cnt.flop += 2;
