@@ -515,13 +515,33 @@ __device__ __forceinline__ vec3 mengersponge(vec3 p) {
         // needs it, and leaves d and res unchanged on the lanes past their exit;
         // a per-lane break was if-converted, every fold computed on every call)
         if (__builtin_amdgcn_ballot_w64(d < 1.0f / (s * 3.0f)) == 0) break;
-        vec3 a = mod(p * s, 2.0f) - 1.0f;
+        // r = abs(1 - 3 abs(mod(p s, 2) - 1)) as rm_device.h sponge_folds forms it
+        // (round 5: 29 -> ~17 VALU per fold in the probe instance).  With
+        // h = x (s/2) (exact: s/2 is a power of 3 over 2 and x s / 2 = RN(x s) / 2),
+        // the exact instance's mod(x s, 2) - 1 is fma(2, h - floor(h), -1), the
+        // same bits as the GLSL's x s - 2 floor(x s / 2) - 1 (one rounding);
+        // the probe instance uses |mod(x s, 2) - 1| = 2 |g|, g = y - rint(y),
+        // y = x s/2 - 1/2 (the distance to the nearest k + 1/2), one fma less
+        // and no floor.  min(max(rx, ry), max(ry, rz), max(rz, rx)) is their
+        // median (v_med3).
+        const float sh = s * 0.5f;
+        vec3 r;
+        if (RM_LIB_PROBE) {
+            const float yx = fmaf(p.x, sh, -0.5f), yy = fmaf(p.y, sh, -0.5f), yz = fmaf(p.z, sh, -0.5f);
+            r = vec3(fabsf(fmaf(-6.0f, fabsf(yx - __builtin_rintf(yx)), 1.0f)),
+                     fabsf(fmaf(-6.0f, fabsf(yy - __builtin_rintf(yy)), 1.0f)),
+                     fabsf(fmaf(-6.0f, fabsf(yz - __builtin_rintf(yz)), 1.0f)));
+        } else {
+            const float hx = p.x * sh, hy = p.y * sh, hz = p.z * sh;
+            r = vec3(fabsf(1.0f - 3.0f * fabsf(fmaf(2.0f, hx - floorf(hx), -1.0f))),
+                     fabsf(1.0f - 3.0f * fabsf(fmaf(2.0f, hy - floorf(hy), -1.0f))),
+                     fabsf(1.0f - 3.0f * fabsf(fmaf(2.0f, hz - floorf(hz), -1.0f))));
+        }
         s *= 3.0f;
-        vec3 r = abs(1.0f - 3.0f * abs(a));
         float da = max(r.x, r.y);
         float db = max(r.y, r.z);
         float dc = max(r.z, r.x);
-        float c = div_k(min(da, min(db, dc)) - 1.0f, s);
+        float c = div_k(__builtin_amdgcn_fmed3f(r.x, r.y, r.z) - 1.0f, s);
         if (c > d) {
             d = c;
             res = vec3(d, 0.2f * da * db * dc, (1.0f + (float)m) / 4.0f);
