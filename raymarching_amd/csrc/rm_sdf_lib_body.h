@@ -176,7 +176,11 @@ __device__ __forceinline__ float dot(vec2 a, vec2 b) { return a.x * b.x + a.y * 
 __device__ __forceinline__ float dot(vec4 a, vec4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
 __device__ __forceinline__ float length(vec2 a) { return sqrt(dot(a, a)); }
 // |a| of a vec3 in the library's shapes (rm::length, or the hardware square root in the probe instance)
-__device__ __forceinline__ float len3_(vec3 a) { return RM_LIB_PROBE ? __builtin_amdgcn_sqrtf(dot(a, a)) : length(a); }
+// (the probe form's sum of squares as explicit FMAs: rm_device.h's dot of the
+// shared vec3 lies outside this instance's contraction pragma)
+__device__ __forceinline__ float len3_(vec3 a) {
+    return RM_LIB_PROBE ? __builtin_amdgcn_sqrtf(fmaf(a.z, a.z, fmaf(a.y, a.y, a.x * a.x))) : length(a);
+}
 __device__ __forceinline__ float distance(vec3 a, vec3 b) { return length(a - b); }
 __device__ __forceinline__ vec2 normalize(vec2 a) { return a * (1.0f / length(a)); }
 // dot, length, normalize, reflect and refract of vec3 are rm_device.h's (found
@@ -337,13 +341,23 @@ __device__ __forceinline__ Rot rot_of(float angle_deg) {  // cos / sin as rotati
     float a = radians(angle_deg);
     return Rot{cos(a), sin(a)};
 }
+// The probe instance drops a rotation whose sine is a compile-time zero (an
+// angle of 0 in the scene source: the cosine is then 1, the product the
+// identity); the exact instance keeps the GLSL's products (x * 0 is not
+// foldable in IEEE arithmetic).
+__device__ __forceinline__ bool rot_is_identity(Rot r) {
+    return RM_LIB_PROBE && __builtin_constant_p(r.s) && __builtin_constant_p(r.c) && r.s == 0.0f && r.c == 1.0f;
+}
 __device__ __forceinline__ vec4 mul_rx(vec4 v, Rot r) {  // v * rotationX
+    if (rot_is_identity(r)) return v;
     return vec4(v.x, v.y * r.c + v.z * -r.s, v.y * r.s + v.z * r.c, v.w);
 }
 __device__ __forceinline__ vec4 mul_ry(vec4 v, Rot r) {  // v * rotationY
+    if (rot_is_identity(r)) return v;
     return vec4(v.x * r.c + v.z * r.s, v.y, v.x * -r.s + v.z * r.c, v.w);
 }
 __device__ __forceinline__ vec4 mul_rz(vec4 v, Rot r) {  // v * rotationZ
+    if (rot_is_identity(r)) return v;
     return vec4(v.x * r.c + v.y * -r.s, v.x * r.s + v.y * r.c, v.z, v.w);
 }
 __device__ __forceinline__ vec4 mul_t(vec4 v, vec3 pos) {  // v * translation_inv(pos)
