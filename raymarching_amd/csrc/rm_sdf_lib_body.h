@@ -82,8 +82,16 @@ __device__ __forceinline__ float max(float x, float y) { return __builtin_elemen
 // Markstein correction of x * RN(1/k) (rm_device.h div_const), the correctly
 // rounded quotient (checked exhaustively over two binades of x for the
 // library's divisors), 3 VALU instead of the ~12 of the IEEE division.
+// A power-of-two divisor (k = 0.5 in the smooth minima of most scenes) is one
+// multiplication by its exact reciprocal in both instances: x * (1/k) is then
+// the exact quotient rounded once, the IEEE division's bits.
+__device__ __forceinline__ constexpr bool pow2_normal(float k) {
+    return k > 0.0f && (__builtin_bit_cast(unsigned, k) & 0x7FFFFFu) == 0u &&
+           (__builtin_bit_cast(unsigned, k) >> 23) > 1u && (__builtin_bit_cast(unsigned, k) >> 23) < 254u;
+}
 __device__ __forceinline__ float div_k(float x, float k) {
     if (RM_LIB_PROBE) return __builtin_constant_p(k) ? x * (1.0f / k) : x * __builtin_amdgcn_rcpf(k);
+    if (__builtin_constant_p(k) && pow2_normal(k)) return x * (1.0f / k);
     return __builtin_constant_p(k) ? div_const(x, k, 1.0f / k) : x / k;
 }
 __device__ __forceinline__ float clamp(float x, float lo, float hi) { return min(max(x, lo), hi); }
