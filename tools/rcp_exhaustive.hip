@@ -3,7 +3,7 @@
 // the correctly rounded 1/x for every float x in [lo, hi)?  Compared on the
 // GPU against the IEEE division of a translation unit built with
 // -fhip-fp32-correctly-rounded-divide-sqrt.  Used to replace post.frag's
-// rcpDirMin = 1.0 / (...) in rm_fxaa (rm_post.hip) whose argument lies in
+// rcpDirMin = 1.0 / (...) in rm_fxaa (rm_fxaa.hip) whose argument lies in
 // [1/128, 2.125]: prints the mismatch count (and the first mismatches).
 // Build: hipcc --offload-arch=gfx950 -O3 -fhip-fp32-correctly-rounded-divide-sqrt \
 //        tools/rcp_exhaustive.hip -o tools/rcp_exhaustive
