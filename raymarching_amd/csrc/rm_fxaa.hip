@@ -119,6 +119,9 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #ifndef RM_FXAA_LINEAR
 #define RM_FXAA_LINEAR 0
 #endif
+#ifndef RM_FXAA_GTAP
+#define RM_FXAA_GTAP 0
+#endif
 constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
 constexpr int FXL_MAX_DIM = 1 << 20;
 static_assert((FXL_TY & (FXL_TY - 1)) == 0 && FXL_TY <= 64, "fy_lane: one lane per tile row");
@@ -142,7 +145,9 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     __shared__ float4 sf4[FXL_H * FXL_W];
     __shared__ uint8_t salpha[FXL_H * FXL_W];
 #else
+#if !RM_FXAA_GTAP
     __shared__ uint32_t stex[FXL_H * FXL_W];
+#endif
     __shared__ float slum[FXL_H * FXL_W];
 #endif
     const int x0 = blockIdx.x * FXL_TX, y0 = blockIdx.y * FXL_TY;
@@ -206,10 +211,14 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
                 salpha[r * FXL_W + 64 + lane] = (uint8_t)(t1[k] >> 24);
             }
 #else
+#if !RM_FXAA_GTAP
             stex[r * FXL_W + lane] = t0[k];
+#endif
             slum[r * FXL_W + lane] = luma(rgb(t0[k]));
             if (lane < FXL_W - 64) {
+#if !RM_FXAA_GTAP
                 stex[r * FXL_W + 64 + lane] = t1[k];
+#endif
                 slum[r * FXL_W + 64 + lane] = luma(rgb(t1[k]));
             }
 #endif
@@ -224,7 +233,12 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     const float fx = ((float)x + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
     // a span tap: post.frag's float address (NEAREST), then the staged texel
     // (block row * FXL_W as a 24-bit multiply: the row is clamped into the block)
-#if RM_FXAA_F4
+#if RM_FXAA_GTAP
+    // RM_FXAA_GTAP: the span taps read the frame (L1/L2: the block was just
+    // loaded), NEAREST + CLAMP_TO_EDGE as texel() forms it; LDS holds only the
+    // lumas (12 KB a workgroup: eight waves per SIMD instead of six)
+    auto span_tap = [&](float u, float v) -> RGB { return rgb(texel(in, W, H, u, v)); };
+#elif RM_FXAA_F4
     const int blk0 = -(ty0 * FXL_W + tx0);  // (the bound above keeps every span texel inside the block)
     auto span_tap = [&](float u, float v) -> RGB {
         const float4 t = sf4[__mul24(floor_i32(v * (float)H), FXL_W) + floor_i32(u * (float)W) + blk0];
@@ -267,7 +281,11 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
 #else
         const float lNW = slum[m - FXL_W - 1], lNE = slum[m - FXL_W + 1], lSW = slum[m + FXL_W - 1];
         const float lSE = slum[m + FXL_W + 1], lM = slum[m];
+#if RM_FXAA_GTAP
+        const uint32_t tM = in[(size_t)(H - 1 - y) * W + (x < W ? x : W - 1)];  // (the centre texel, stex[m])
+#else
         const uint32_t tM = stex[m];
+#endif
 #endif
         const float fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_lane), ly));
         // (lumas are never NaN or -0: IEEE minimum/maximum, v_minimum3/v_maximum3,
