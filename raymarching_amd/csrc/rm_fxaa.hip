@@ -122,9 +122,32 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #ifndef RM_FXAA_GTAP
 #define RM_FXAA_GTAP 0
 #endif
-constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = 5, FXL_W = FXL_TX + 2 * FXL_HALO, FXL_H = FXL_TY + 2 * FXL_HALO;
+// RM_FXAA_HALO: the span texels lie within +-4 of the pixel (above), so a
+// halo of 4 holds them all; RM_FXAA_TRIM: lumas only for the texels the +-1
+// taps read, (TX + 2) x (TY + 2), not the whole block; RM_FXAA_NW: waves per
+// workgroup (LDS per workgroup and the 32-waves-per-CU cap set the occupancy)
+#ifndef RM_FXAA_HALO
+#define RM_FXAA_HALO 5
+#endif
+#ifndef RM_FXAA_TRIM
+#define RM_FXAA_TRIM 0
+#endif
+#ifndef RM_FXAA_NW
+#define RM_FXAA_NW 4
+#endif
+constexpr int FXL_TX = 64, FXL_TY = RM_FXAA_TY, FXL_HALO = RM_FXAA_HALO, FXL_W = FXL_TX + 2 * FXL_HALO,
+              FXL_H = FXL_TY + 2 * FXL_HALO;
+constexpr int FXL_NW = RM_FXAA_NW, FXL_NT = 64 * FXL_NW;
+#if RM_FXAA_TRIM
+constexpr int SL_W = FXL_TX + 2, SL_H = FXL_TY + 2, SL_O = FXL_HALO - 1;  // luma region: block (SL_O, SL_O) on
+static_assert(!RM_FXAA_LINEAR && !RM_FXAA_F4 && !RM_FXAA_GTAP, "RM_FXAA_TRIM: column staging only");
+#else
+constexpr int SL_W = FXL_W, SL_H = FXL_H, SL_O = 0;
+#endif
 constexpr int FXL_MAX_DIM = 1 << 20;
+static_assert(FXL_HALO >= 4 && FXL_W - 64 <= 64, "span texels within +-4; two staging columns per lane");
 static_assert((FXL_TY & (FXL_TY - 1)) == 0 && FXL_TY <= 64, "fy_lane: one lane per tile row");
+static_assert(FXL_TY % (RM_FXAA_ROWS * FXL_NW) == 0, "whole passes of RM_FXAA_ROWS rows per wave");
 __device__ __forceinline__ int clamp_to(int v, int hi) {  // v_med3_i32(v, 0, hi)
     int r;
     asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "v"(hi));
@@ -135,7 +158,7 @@ __device__ __forceinline__ int floor_i32(float v) {  // (int)floorf(v) for |v| <
     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
     return r;
 }
-__global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                           int W, int H) {
 #if RM_FXAA_F4
     // RM_FXAA_F4: each staged texel as the floats GL reads (r, g, b) and its
@@ -148,7 +171,7 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
 #if !RM_FXAA_GTAP
     __shared__ uint32_t stex[FXL_H * FXL_W];
 #endif
-    __shared__ float slum[FXL_H * FXL_W];
+    __shared__ float slum[SL_H * SL_W];
 #endif
     const int x0 = blockIdx.x * FXL_TX, y0 = blockIdx.y * FXL_TY;
     // output rows y0 .. y0 + TY - 1 read texel rows H-1-y (+-1, span): the block
@@ -164,11 +187,11 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     // (the column layout above loads 22 words per lane and forms the lumas of
     // the last ten columns in full-wave instructions for ten lanes)
     {
-        constexpr int NT = FXL_H * FXL_W, NP = (NT + 255) / 256;
+        constexpr int NT = FXL_H * FXL_W, NP = (NT + FXL_NT - 1) / FXL_NT;
         uint32_t tt[NP];
 #pragma unroll
         for (int k = 0; k < NP; k++) {
-            const int idx = min((int)threadIdx.x + 256 * k, NT - 1);
+            const int idx = min((int)threadIdx.x + FXL_NT * k, NT - 1);
             const int r = idx / FXL_W, c = idx - r * FXL_W;  // (constant divisor: a multiply-high)
             const int gy = clamp_med3(ty0 + r, H - 1), gx = clamp_med3(tx0 + c, W - 1);
             const uint32_t off = __umul24((uint32_t)gy, (uint32_t)W) + (uint32_t)gx;  // (W, H <= 2^20)
@@ -176,7 +199,7 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
         }
 #pragma unroll
         for (int k = 0; k < NP; k++) {
-            const int idx = (int)threadIdx.x + 256 * k;
+            const int idx = (int)threadIdx.x + FXL_NT * k;
             if (k < NP - 1 || idx < NT) {
                 stex[idx] = tt[k];
                 slum[idx] = luma(rgb(tt[k]));
@@ -184,12 +207,12 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
         }
     }
 #else
-    constexpr int NR = (FXL_H + 3) / 4;
+    constexpr int NR = (FXL_H + FXL_NW - 1) / FXL_NW;
     const int gx0 = clamp_med3(tx0 + lane, W - 1), gx1 = clamp_med3(tx0 + 64 + (lane < FXL_W - 64 ? lane : 0), W - 1);
     uint32_t t0[NR], t1[NR];
 #pragma unroll
     for (int k = 0; k < NR; k++) {
-        const int r = wv + 4 * k;
+        const int r = wv + FXL_NW * k;
         const int gy = clamp_med3(ty0 + (r < FXL_H ? r : FXL_H - 1), H - 1);
         // one 32-bit byte offset from the kernel-argument base per load (the
         // saddr form: no 64-bit address add; frames < 2^30 texels)
@@ -199,7 +222,7 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     }
 #pragma unroll
     for (int k = 0; k < NR; k++) {
-        const int r = wv + 4 * k;
+        const int r = wv + FXL_NW * k;
         if (r < FXL_H) {
 #if RM_FXAA_F4
             const RGB c0 = rgb(t0[k]);
@@ -213,13 +236,12 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
 #else
 #if !RM_FXAA_GTAP
             stex[r * FXL_W + lane] = t0[k];
+            if (lane < FXL_W - 64) stex[r * FXL_W + 64 + lane] = t1[k];
 #endif
-            slum[r * FXL_W + lane] = luma(rgb(t0[k]));
-            if (lane < FXL_W - 64) {
-#if !RM_FXAA_GTAP
-                stex[r * FXL_W + 64 + lane] = t1[k];
-#endif
-                slum[r * FXL_W + 64 + lane] = luma(rgb(t1[k]));
+            const int lr = r - SL_O;  // (wave-uniform)
+            if (lr >= 0 && lr < SL_H) {
+                if (lane >= SL_O) slum[lr * SL_W + lane - SL_O] = luma(rgb(t0[k]));
+                if (lane < FXL_W - 64 && 64 + lane - SL_O < SL_W) slum[lr * SL_W + 64 + lane - SL_O] = luma(rgb(t1[k]));
             }
 #endif
         }
@@ -273,14 +295,16 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     // clamped row and not stored)
     auto pixel = [&](int ly) -> uint32_t {
         const int y = min(y0 + ly, H - 1);
-        const int m = (FXL_TY - 1 - (y - y0) + FXL_HALO) * FXL_W + (lane + FXL_HALO);
+        const int rr = FXL_TY - 1 - (y - y0);  // block row of the pixel's texel, less the halo
+        const int m = (rr + FXL_HALO) * FXL_W + (lane + FXL_HALO);
+        const int ml = (rr + FXL_HALO - SL_O) * SL_W + (lane + FXL_HALO - SL_O);
 #if RM_FXAA_F4
         const float lNW = sf4[m - FXL_W - 1].w, lNE = sf4[m - FXL_W + 1].w, lSW = sf4[m + FXL_W - 1].w;
         const float lSE = sf4[m + FXL_W + 1].w, lM = sf4[m].w;
         const uint32_t tM = (uint32_t)salpha[m] << 24;
 #else
-        const float lNW = slum[m - FXL_W - 1], lNE = slum[m - FXL_W + 1], lSW = slum[m + FXL_W - 1];
-        const float lSE = slum[m + FXL_W + 1], lM = slum[m];
+        const float lNW = slum[ml - SL_W - 1], lNE = slum[ml - SL_W + 1], lSW = slum[ml + SL_W - 1];
+        const float lSE = slum[ml + SL_W + 1], lM = slum[ml];
 #if RM_FXAA_GTAP
         const uint32_t tM = in[(size_t)(H - 1 - y) * W + (x < W ? x : W - 1)];  // (the centre texel, stex[m])
 #else
@@ -330,18 +354,19 @@ __global__ __launch_bounds__(256) void rm_fxaa_lds_kernel(const uint32_t* __rest
     // RM_FXAA_ROWS rows at a time: their dependent chains (LDS taps -> division
     // -> span taps) interleave
 #if RM_FXAA_ROWS == 4
-    for (int ly = wv; ly < FXL_TY; ly += 16) {
-        const uint32_t v0 = pixel(ly), v1 = pixel(ly + 4), v2 = pixel(ly + 8), v3 = pixel(ly + 12);
+    constexpr int N = FXL_NW;
+    for (int ly = wv; ly < FXL_TY; ly += 4 * N) {
+        const uint32_t v0 = pixel(ly), v1 = pixel(ly + N), v2 = pixel(ly + 2 * N), v3 = pixel(ly + 3 * N);
         if (x < W && y0 + ly < H) out[(size_t)(y0 + ly) * W + x] = v0;
-        if (x < W && y0 + ly + 4 < H) out[(size_t)(y0 + ly + 4) * W + x] = v1;
-        if (x < W && y0 + ly + 8 < H) out[(size_t)(y0 + ly + 8) * W + x] = v2;
-        if (x < W && y0 + ly + 12 < H) out[(size_t)(y0 + ly + 12) * W + x] = v3;
+        if (x < W && y0 + ly + N < H) out[(size_t)(y0 + ly + N) * W + x] = v1;
+        if (x < W && y0 + ly + 2 * N < H) out[(size_t)(y0 + ly + 2 * N) * W + x] = v2;
+        if (x < W && y0 + ly + 3 * N < H) out[(size_t)(y0 + ly + 3 * N) * W + x] = v3;
     }
 #else
-    for (int ly = wv; ly < FXL_TY; ly += 8) {
-        const uint32_t v0 = pixel(ly), v1 = pixel(ly + 4);
+    for (int ly = wv; ly < FXL_TY; ly += 2 * FXL_NW) {
+        const uint32_t v0 = pixel(ly), v1 = pixel(ly + FXL_NW);
         if (x < W && y0 + ly < H) out[(size_t)(y0 + ly) * W + x] = v0;
-        if (x < W && y0 + ly + 4 < H) out[(size_t)(y0 + ly + 4) * W + x] = v1;
+        if (x < W && y0 + ly + FXL_NW < H) out[(size_t)(y0 + ly + FXL_NW) * W + x] = v1;
     }
 #endif
 }
@@ -353,7 +378,7 @@ hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStrea
     if (W <= 0 || H <= 0) return hipSuccess;
     if (RM_FXAA_LDS && W <= FXL_MAX_DIM && H <= FXL_MAX_DIM) {
         dim3 grid((W + FXL_TX - 1) / FXL_TX, (H + FXL_TY - 1) / FXL_TY);
-        hipLaunchKernelGGL(rm_fxaa_lds_kernel, grid, dim3(256), 0, s, in, out, W, H);
+        hipLaunchKernelGGL(rm_fxaa_lds_kernel, grid, dim3(FXL_NT), 0, s, in, out, W, H);
         return hipGetLastError();
     }
     dim3 grid((W + FXAA_TX - 1) / FXAA_TX, (H + FXAA_TY - 1) / FXAA_TY);
