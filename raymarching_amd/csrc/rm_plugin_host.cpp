@@ -212,7 +212,8 @@ std::string translation_unit(const std::string& src, const std::string& file) {
            instance("namespace rm {\nnamespace glsl {\n", "}  // namespace glsl\n}  // namespace rm\n", "", "") +
            instance("namespace rm {\nnamespace glsl {\nnamespace probe {\n",
                     "}  // namespace probe\n}  // namespace glsl\n}  // namespace rm\n",
-                    "#pragma clang fp contract(fast)\n", "#pragma clang fp contract(off)\n") +
+                    "#pragma clang fp contract(fast)\n#if RM_PROBE_REASSOC\n#pragma clang fp reassociate(on)\n#endif\n",
+                    "#if RM_PROBE_REASSOC\n#pragma clang fp reassociate(off)\n#endif\n#pragma clang fp contract(off)\n") +
            "#include \"rm_plugin_kernels.h\"\n";
 }
 
