@@ -94,7 +94,11 @@ struct rm_ctx {
         uint64_t k = 0;            // launches so far
         uint32_t *buf = nullptr;   // cost[2][n] | order[2][n] | 2 x (hist[256] | cursor[256]) | bucket u8[n]
         hipEvent_t last = nullptr;  // after the last launch that read or wrote buf: recorded on `stream`
-        bool dirty = false;         // when the context leaves the stream or the entry is released
+        bool dirty = false;         // when the entry is released or the context destroyed on `stream`
+        // ... or, once the context has left `stream`, the `done` event recorded
+        // there as it left (borrowed: one marker per leave instead of one per
+        // entry as well; rm_destroy destroys it after the entries are released)
+        hipEvent_t left = nullptr;
         uint64_t used = 0;
     };
     Sched sched[8];
@@ -126,13 +130,14 @@ rm_status mark_done(rm_ctx *ctx) {
 }
 
 // Record the adaptive-order entries' `last` events still owed on the ctx
-// stream (before the context leaves it, or releases an entry of it).
+// stream (before the context is destroyed).
 hipError_t record_sched_last(rm_ctx *ctx) {
     for (rm_ctx::Sched &e : ctx->sched)
         if (e.buf && e.dirty && e.stream == ctx->stream) {
             hipError_t r = hipEventRecord(e.last, ctx->stream);
             if (r != hipSuccess) return r;
             e.dirty = false;
+            e.left = nullptr;
         }
     return hipSuccess;
 }
@@ -468,8 +473,17 @@ int pick_kernel(const rm_ctx *c) {
 hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
     hipError_t r = hipSuccess;
     if (e.buf) {
-        if (e.dirty && e.stream == ctx->stream) r = hipEventRecord(e.last, ctx->stream);
-        if (r == hipSuccess && e.last) r = hipEventSynchronize(e.last);
+        if (e.dirty && e.stream == ctx->stream) {
+            r = hipEventRecord(e.last, ctx->stream);
+            if (r == hipSuccess) r = hipEventSynchronize(e.last);
+        } else if (e.left) {
+            // the context left e.stream after e's last launch: the marker
+            // recorded then (a `done` event, re-recorded later only once it had
+            // completed, so a wait on it never returns early)
+            r = hipEventSynchronize(e.left);
+        } else if (e.last) {
+            r = hipEventSynchronize(e.last);
+        }
         (void)hipFree(e.buf);
     }
     if (e.last) (void)hipEventDestroy(e.last);
@@ -579,7 +593,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
         if (e != hipSuccess) return hip_fail(ctx, e, "tile order launch");
     }
     if (sc) {
-        sc->dirty = true;  // (its `last` event is recorded when the context leaves the stream)
+        sc->dirty = true;  // (marked when the context leaves the stream: rm_set_stream)
         if (!cnt) sc->k++;
     }
     rm_status ms_st = mark_done(ctx);
@@ -765,8 +779,10 @@ rm_status rm_destroy(rm_ctx *ctx) {
     }
     for (auto &b : ctx->persist)
         if (b.last) (void)hipEventSynchronize(b.last);
-    for (rm_ctx::Sched &e : ctx->sched)
-        if (e.buf && e.last) (void)hipEventSynchronize(e.last);
+    for (rm_ctx::Sched &e : ctx->sched) {
+        if (e.buf && e.last && !e.left) (void)hipEventSynchronize(e.last);
+        e.left = nullptr;  // (its `done` event was waited for above and is destroyed)
+    }
     rmplugin::unload(ctx->plugin);
     if (ctx->d_evals) (void)hipFree(ctx->d_evals);
     for (auto &b : ctx->persist) {
@@ -879,13 +895,31 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *p) {
 rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // RM_LEAVE_NO_RECORD=1 (analysis only, unsafe: a later release or realloc
+    // of a schedule buffer no longer waits for the old stream's work): leaving
+    // a stream records nothing, to price the two markers (tools/scale_model.py)
+    static const bool no_record = [] {
+        const char* e = std::getenv("RM_LEAVE_NO_RECORD");
+        return e && e[0] == '1';
+    }();
+    if (no_record) {
+        ctx->stream = s;
+        return RM_OK;
+    }
     if (s != ctx->stream && ctx->dirty) {
-        // the old stream's last-work events, recorded now (it may be gone by
-        // the time they are waited for); `done` is kept until it completes,
-        // a completed one is reused for the new stream (no host wait here)
+        // the old stream's last work, marked now (it may be gone by the time it
+        // is waited for): one `done` event, which the adaptive-order entries
+        // used there since borrow (a second marker per leave cost ~4 us of
+        // every frame on the two-stream pipeline); `done` is
+        // kept until it completes, a completed one is reused for the new
+        // stream (no host wait here)
         RM_HIP(hipSetDevice(ctx->device));
-        RM_HIP(record_sched_last(ctx));
         RM_HIP(hipEventRecord(ctx->done, ctx->stream));
+        for (rm_ctx::Sched &e : ctx->sched)
+            if (e.buf && e.dirty && e.stream == ctx->stream) {
+                e.left = ctx->done;
+                e.dirty = false;
+            }
         hipEvent_t next = nullptr;
         for (size_t i = 0; i < ctx->retired.size(); i++)
             if (hipEventQuery(ctx->retired[i]) == hipSuccess) {

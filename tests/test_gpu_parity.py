@@ -1084,3 +1084,32 @@ def test_context_outlives_a_destroyed_stream(torch_cuda):
     assert torch.equal(out2, ref)
     r.close()
 
+
+
+@pytest.mark.gpu
+def test_schedule_entries_released_after_their_stream_was_left(torch_cuda):
+    """Leaving a stream records one marker, `done`, which the adaptive-order
+    entries used there borrow.  Ten geometries on two
+    alternating streams cycle the eight entries, so entries of a left stream
+    are released (least recently used) while their borrowed marker has been
+    re-recorded for later leaves; every frame must still be right."""
+    torch = torch_cuda
+    r = rm.Renderer(0)
+    setup(r, "T", POSES["P2"], 64)
+    r.set_params(count_evals=0, schedule=1)
+    sizes = [(64, 40 + 2 * i) for i in range(10)]
+    refs = {s: r.render_rgba8(*s).clone() for s in sizes}
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = []
+    for it in range(3):
+        for k, s in enumerate(sizes):
+            st = streams[(k + it) % 2]
+            with torch.cuda.stream(st):
+                r.set_stream(st)
+                outs.append((it, s, r.render_rgba8(*s)))
+    r.set_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    for it, s, o in outs:
+        assert torch.equal(o, refs[s]), (it, s)
+    r.close()
