@@ -164,7 +164,8 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *params);
 /* Stream the ctx launches on (a hipStream_t; NULL = the null stream).
  * Lifetime: a stream must outlive its binding.  Before destroying a stream the
  * context is bound to, bind another one (e.g. rm_set_stream(ctx, NULL)): that
- * records the context's completion events on the old stream while it exists.
+ * records the context's completion marker (one event, only when the context
+ * enqueued work there since it was bound) on the old stream while it exists.
  * Streams the context has left may be destroyed at any time.  Destroying the
  * bound stream first is undefined behaviour: the HIP runtime does not validate
  * stream handles, and a later rm_* call (rm_destroy included) that records on
