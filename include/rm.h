@@ -171,6 +171,14 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *params);
  * stream handles, and a later rm_* call (rm_destroy included) that records on
  * the freed stream crashed the process in a test (SIGSEGV inside libamdhip64). */
 rm_status rm_set_stream(rm_ctx *ctx, void *hip_stream);
+/* rm_set_stream, with the caller's promise that the stream stays alive until
+ * rm_destroy (e.g. a stream of PyTorch's pool, which is never destroyed).
+ * Leaving a kept stream then records nothing on it; the context marks its work
+ * there only when something waits for it (rm_destroy, or reusing a schedule
+ * buffer), on the stream itself.  A frame loop that alternates between two
+ * kept streams saves one marker per frame (~4 us each on MI355X, DESIGN.md
+ * 2.14).  (No counterpart in the reference, which draws on one GL context.) */
+rm_status rm_set_stream_kept(rm_ctx *ctx, void *hip_stream);
 rm_status rm_synchronize(rm_ctx *ctx);
 
 /* Replaces renderTexture.draw(sprite, &shader) (main.cpp:199,205): run the

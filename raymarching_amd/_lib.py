@@ -19,7 +19,8 @@ STATUS_CODES = {v: k for k, v in STATUS.items()}
 
 # every symbol include/rm.h declares
 EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_set_uniform2f",
-           "rm_set_uniform3f", "rm_set_params", "rm_get_params", "rm_set_stream", "rm_synchronize",
+           "rm_set_uniform3f", "rm_set_params", "rm_get_params", "rm_set_stream", "rm_set_stream_kept",
+           "rm_synchronize",
            "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8",
            "rm_pack_rgba8", "rm_pack_rgb8", "rm_deinterleave_rgb8",
            "rm_render_rgba8", "rm_render_accumulate", "rm_render_accumulate_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_last_error", "rm_status_string",
@@ -98,6 +99,7 @@ def lib() -> ctypes.CDLL:
         "rm_set_params": ([vp, c.POINTER(RmParams)], c.c_int),
         "rm_get_params": ([vp, c.POINTER(RmParams)], c.c_int),
         "rm_set_stream": ([vp, vp], c.c_int),
+        "rm_set_stream_kept": ([vp, vp], c.c_int),
         "rm_synchronize": ([vp], c.c_int),
         "rm_render": ([vp, c.c_int, c.c_int, vp, c.POINTER(RmStats)], c.c_int),
         "rm_render_step_map": ([vp, c.c_int, c.c_int, vp, vp, c.POINTER(RmStats)], c.c_int),

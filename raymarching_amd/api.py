@@ -95,10 +95,13 @@ class Renderer:
         check(lib().rm_get_params(self._ctx, ctypes.byref(p)), self._ctx)
         return p
 
-    def set_stream(self, stream) -> None:
-        """stream: a torch.cuda.Stream, a raw hipStream_t int, or None."""
+    def set_stream(self, stream, kept: bool = False) -> None:
+        """stream: a torch.cuda.Stream, a raw hipStream_t int, or None.  kept:
+        the stream outlives this renderer (rm_set_stream_kept; PyTorch's pool
+        streams are never destroyed), so leaving it records no marker."""
         raw = getattr(stream, "cuda_stream", stream)
-        check(lib().rm_set_stream(self._ctx, ctypes.c_void_p(raw or 0)), self._ctx)
+        fn = lib().rm_set_stream_kept if kept else lib().rm_set_stream
+        check(fn(self._ctx, ctypes.c_void_p(raw or 0)), self._ctx)
 
     def tile_grid(self, W: int, rows: int) -> tuple:
         """(tiles_x, tiles_y) of a render launch over W x rows pixels."""

@@ -62,6 +62,11 @@ struct rm_ctx {
     hipEvent_t done = nullptr;
     bool dirty = false;
     std::vector<hipEvent_t> retired;
+    // streams bound with rm_set_stream_kept (the caller keeps them alive until
+    // rm_destroy): leaving one records nothing; it joins `owed`, and its work
+    // is marked only when something waits for it (an entry's release,
+    // rm_destroy), on the stream itself
+    std::vector<hipStream_t> kept, owed;
     float sample_part = 1.0f;  // u_sample_part, u_seed1, u_seed2: read by rm_render_accumulate*
     float seed1[2] = {0.0f, 0.0f}, seed2[2] = {0.0f, 0.0f};
     rm_params params = {128, 0, 0, 0, 1};
@@ -124,17 +129,23 @@ rm_status hip_fail(rm_ctx *c, hipError_t e, const char *what) {
     } while (0)
 
 // Note that the context enqueued work on its stream (rm_ctx::dirty).
+bool is_kept(const rm_ctx *ctx, hipStream_t s) {
+    for (hipStream_t k : ctx->kept)
+        if (k == s) return true;
+    return false;
+}
+
 rm_status mark_done(rm_ctx *ctx) {
     ctx->dirty = true;
     return RM_OK;
 }
 
 // Record the adaptive-order entries' `last` events still owed on the ctx
-// stream (before the context is destroyed).
+// stream or on a kept stream (before the context is destroyed).
 hipError_t record_sched_last(rm_ctx *ctx) {
     for (rm_ctx::Sched &e : ctx->sched)
-        if (e.buf && e.dirty && e.stream == ctx->stream) {
-            hipError_t r = hipEventRecord(e.last, ctx->stream);
+        if (e.buf && e.dirty && (e.stream == ctx->stream || is_kept(ctx, e.stream))) {
+            hipError_t r = hipEventRecord(e.last, e.stream);
             if (r != hipSuccess) return r;
             e.dirty = false;
             e.left = nullptr;
@@ -473,8 +484,8 @@ int pick_kernel(const rm_ctx *c) {
 hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
     hipError_t r = hipSuccess;
     if (e.buf) {
-        if (e.dirty && e.stream == ctx->stream) {
-            r = hipEventRecord(e.last, ctx->stream);
+        if (e.dirty && (e.stream == ctx->stream || is_kept(ctx, e.stream))) {
+            r = hipEventRecord(e.last, e.stream);
             if (r == hipSuccess) r = hipEventSynchronize(e.last);
         } else if (e.left) {
             // the context left e.stream after e's last launch: the marker
@@ -769,6 +780,11 @@ rm_status rm_destroy(rm_ctx *ctx) {
         if (hipEventRecord(ctx->done, ctx->stream) == hipSuccess) (void)hipEventSynchronize(ctx->done);
         else lost = true;
     }
+    for (hipStream_t s : ctx->owed)  // kept streams left with this context's work on them
+        if (!lost && ctx->done) {
+            if (hipEventRecord(ctx->done, s) == hipSuccess) (void)hipEventSynchronize(ctx->done);
+            else lost = true;
+        }
     if (lost) {
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
@@ -906,6 +922,13 @@ rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
         ctx->stream = s;
         return RM_OK;
     }
+    if (s != ctx->stream && ctx->dirty && is_kept(ctx, ctx->stream)) {
+        // a kept stream: no marker now (its entries stay dirty, rm_ctx::kept)
+        bool listed = false;
+        for (hipStream_t o : ctx->owed) listed = listed || o == ctx->stream;
+        if (!listed) ctx->owed.push_back(ctx->stream);
+        ctx->dirty = false;
+    }
     if (s != ctx->stream && ctx->dirty) {
         // the old stream's last work, marked now (it may be gone by the time it
         // is waited for): one `done` event, which the adaptive-order entries
@@ -935,6 +958,13 @@ rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
     }
     ctx->stream = s;
     return RM_OK;
+}
+
+rm_status rm_set_stream_kept(rm_ctx *ctx, void *stream) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!is_kept(ctx, s)) ctx->kept.push_back(s);
+    return rm_set_stream(ctx, stream);
 }
 
 rm_status rm_synchronize(rm_ctx *ctx) {

@@ -374,6 +374,13 @@ class DistributedFrame:
             self.r.deinterleave(p.W, p.H, p.band, p.nshards, p.rows_per_shard, self.gathered[slot],
                                 out=self.frames[slot])
 
+    def _bind(self, st):
+        """Bind the renderer to frame stream st.  The frame streams other than
+        the caller's come from PyTorch's pool, which never destroys them, so
+        they are bound as kept (rm_set_stream_kept): leaving one records no
+        marker."""
+        self.r.set_stream(st, kept=st is not self.caller)
+
     def render_local(self, stats=False):
         """This rank's rows only, into slot 0 (no gather), on the first frame
         stream (whose adaptive tile order the frames use); stats: one
@@ -382,7 +389,7 @@ class DistributedFrame:
         dst = self.wires[0] if self.locals is None else self.locals[0]
         st = self.streams[0]
         with torch.cuda.stream(st):
-            self.r.set_stream(st)
+            self._bind(st)
             try:
                 res = self._render_into(dst, 0, self.nmine, stats=stats)
             finally:
@@ -403,7 +410,7 @@ class DistributedFrame:
         nch = len(self.cuts) - 1
         works = []
         with torch.cuda.stream(st):  # the collectives order themselves after this stream
-            self.r.set_stream(st)
+            self._bind(st)
             for c in range(nch):
                 self._render_rows(self.cuts[c], self.cuts[c + 1], slot, None if events is None else events[c])
                 if self._pipelined():
@@ -424,7 +431,7 @@ class DistributedFrame:
 
         slot, st, works = item
         with torch.cuda.stream(st):
-            self.r.set_stream(st)
+            self._bind(st)
             for w in works or ():
                 w.wait()  # st waits for the gather
             if self.rank == 0:
@@ -478,7 +485,7 @@ class DistributedFrame:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         self.flush()
         torch.cuda.synchronize(dev)
-        self.r.set_stream(st)
+        self._bind(st)
         with torch.cuda.stream(st):
             ev[0].record(st)
             if self.nmine:
@@ -617,7 +624,7 @@ class DeltaFrame(DistributedFrame):
         import torch
         p = self.plan
         with torch.cuda.stream(st):
-            self.r.set_stream(st)
+            self._bind(st)
             for w in self.slot_works[slot]:  # the slot's previous message has left
                 w.wait()
             self.slot_works[slot] = []
@@ -697,7 +704,7 @@ class DeltaFrame(DistributedFrame):
         self.last_sizes = sizes
         if self.rank == 0:
             with torch.cuda.stream(st):
-                self.r.set_stream(st)
+                self._bind(st)
                 for w in works:
                     w.wait()
                 self._decode(slot, st)
@@ -741,7 +748,7 @@ class DeltaFrame(DistributedFrame):
         import torch
         st = self.streams[0]
         with torch.cuda.stream(st):
-            self.r.set_stream(st)
+            self._bind(st)
             try:
                 res = self._render_into(self.locals[0], 0, self.nmine, stats=stats)
             finally:
@@ -764,7 +771,7 @@ class DeltaFrame(DistributedFrame):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         p = self.plan
         with torch.cuda.stream(st):
-            self.r.set_stream(st)
+            self._bind(st)
             ev[0].record(st)
             if self.nmine:
                 self._render_into(self.locals[slot], 0, self.nmine)
@@ -789,7 +796,7 @@ class DeltaFrame(DistributedFrame):
         out["deinterleave_ms"] = 0.0
         if self.rank == 0:
             with torch.cuda.stream(st):
-                self.r.set_stream(st)
+                self._bind(st)
                 ev[3].record(st)
                 self._decode(slot, st)
                 ev[4].record(st)

@@ -1113,3 +1113,38 @@ def test_schedule_entries_released_after_their_stream_was_left(torch_cuda):
     for it, s, o in outs:
         assert torch.equal(o, refs[s]), (it, s)
     r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("close_on_kept", [False, True])
+def test_kept_streams_frames_and_destroy(torch_cuda, close_on_kept):
+    """rm_set_stream_kept (rm.h): leaving a kept stream records nothing.  The
+    adaptive-order entries used there are marked on the stream itself when
+    they are released (ten geometries over eight entries, on two kept pool
+    streams and the caller's), and rm_destroy marks the kept streams still
+    owed, also while bound to one (close_on_kept).  Every frame must be right."""
+    torch = torch_cuda
+    r = rm.Renderer(0)
+    setup(r, "T", POSES["P2"], 64)
+    r.set_params(count_evals=0, schedule=1)
+    sizes = [(64, 40 + 2 * i) for i in range(10)]
+    refs = {s: r.render_rgba8(*s).clone() for s in sizes}
+    torch.cuda.synchronize()
+    caller = torch.cuda.current_stream()
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = []
+    for it in range(3):
+        for k, s in enumerate(sizes):
+            st = streams[(k + it) % 2]
+            with torch.cuda.stream(st):
+                r.set_stream(st, kept=True)
+                outs.append((it, s, r.render_rgba8(*s)))
+            if k % 3 == 2:  # the caller's (not kept) stream in between
+                r.set_stream(caller)
+                outs.append((it, s, r.render_rgba8(*s)))
+    if not close_on_kept:
+        r.set_stream(caller)
+    r.close()
+    torch.cuda.synchronize()
+    for it, s, o in outs:
+        assert torch.equal(o, refs[s]), (it, s)

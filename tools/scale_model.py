@@ -47,6 +47,7 @@ def cumask_stream(torch):
 
 
 STREAM_KIND = "pool"
+KEPT = False  # --kept: frame streams bound with rm_set_stream_kept, as DistributedFrame binds them
 
 
 def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
@@ -71,10 +72,10 @@ def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
         k = i % nstreams
         st = streams[k]
         with torch.cuda.stream(st):
-            r.set_stream(st)
+            r.set_stream(st, kept=KEPT)
             r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[k])
             r.pack_rgb8(loc[k], out=wire[k])
-        r.set_stream(streams[0])
+        r.set_stream(streams[0], kept=KEPT)
 
     t_end = time.time() + 0.3
     i = 0
@@ -119,13 +120,15 @@ def main():
     ap.add_argument("--band", type=int, default=16)
     ap.add_argument("--streams", type=int, default=2, help="frames in flight per rank (HIP streams)")
     ap.add_argument("--even-only", action="store_true")
+    ap.add_argument("--kept", action="store_true", help="bind the frame streams as kept (no marker per leave)")
     ap.add_argument("--stream-kind", default="probed", choices=["pool", "cumask", "probed"])
     ap.add_argument("--link-gbs", type=float, default=64.0,
                     help="assumed xGMI rate of one link, one direction, as RCCL point-to-point achieves it (GB/s)")
     args = ap.parse_args()
     import torch
-    global STREAM_KIND
+    global STREAM_KIND, KEPT
     STREAM_KIND = args.stream_kind
+    KEPT = args.kept
 
     import raymarching_amd as rm
     from bench import balanced_runs
