@@ -76,8 +76,9 @@ def parse():
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
     ap.add_argument("--streams", type=int, default=None, choices=[1, 2],
                     help="HIP streams frames alternate on (default: 2 for N > 1 over RCCL, else 1; at N = 1 "
-                         "two streams measure ~2 %% faster frames for C3, but each launch then overlaps the next "
-                         "and rocprofv3's per-launch durations no longer equal the kernel's)")
+                         "two streams measure the same C3 frame time (0.4218-0.4220 against 0.4180-0.4225 ms, "
+                         "profiles/r05/n1_streams), and each launch then overlaps the next, so rocprofv3's "
+                         "per-launch durations no longer equal the kernel's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "tile16", "tile8"])
     ap.add_argument("--schedule", default="adaptive", choices=["adaptive", "rowmajor"],
                     help="tile dispatch order: costliest tiles of the previous frame first, or row-major")
