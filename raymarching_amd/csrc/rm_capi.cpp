@@ -911,9 +911,10 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *p) {
 rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // RM_LEAVE_NO_RECORD=1 (analysis only, unsafe: a later release or realloc
-    // of a schedule buffer no longer waits for the old stream's work): leaving
-    // a stream records nothing, to price the two markers (tools/scale_model.py)
+    // RM_LEAVE_NO_RECORD=1 (analysis only, unsafe: a later release of a
+    // schedule buffer or rm_destroy no longer waits for the old stream's
+    // work): leaving a stream records nothing, which prices the marker
+    // (tools/scale_model.py)
     static const bool no_record = [] {
         const char* e = std::getenv("RM_LEAVE_NO_RECORD");
         return e && e[0] == '1';
