@@ -15,6 +15,9 @@
 // Four pixels per lane, 64x16-pixel workgroups (neighbour texels are re-read
 // from L1/L2; 4 B in + 4 B out of HBM per pixel).
 //
+// Rows whose span is short output their centre texel without the span taps
+// (RM_FXAA_FLAT, proof at the test): 0.069-0.072 -> 0.052-0.053 ms on the C3
+// frame, same bits (profiles/r05/fxaa_flat/).
 // Its own translation unit (split from rm_post.hip in round 5) so that it can
 // be scheduled with LLVM's max-ilp strategy, which shortens the latency-bound
 // FXAA kernel (0.0721-0.0729 -> 0.0697-0.0706 ms) but slows bloom's
@@ -121,6 +124,9 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #endif
 #ifndef RM_FXAA_GTAP
 #define RM_FXAA_GTAP 0
+#endif
+#ifndef RM_FXAA_FLAT
+#define RM_FXAA_FLAT 1  // short-span rows output their centre texel (below)
 #endif
 // RM_FXAA_HALO: the span texels lie within +-4 of the pixel (above), so a
 // halo of 4 holds them all; RM_FXAA_TRIM: lumas only for the texels the +-1
@@ -336,8 +342,21 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
 #else
         float rcpDirMin = 1.0f / (fminf(fabsf(dx), fabsf(dy)) + dirReduce);
 #endif
-        dx = __builtin_amdgcn_fmed3f(dx * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX) * ivx;
-        dy = __builtin_amdgcn_fmed3f(dy * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX) * ivy;
+        const float dxs = __builtin_amdgcn_fmed3f(dx * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX);
+        const float dys = __builtin_amdgcn_fmed3f(dy * rcpDirMin, -FXAA_SPAN_MAX, FXAA_SPAN_MAX);
+#if RM_FXAA_FLAT
+        // A short span: with |dxs|, |dys| <= 0.5 texel every span tap (|k| <=
+        // 0.5) lies within 0.25 texel of the pixel centre x + 0.5 (row: H - y -
+        // 0.5), and the roundings of its float address stay below 0.19 texel for
+        // W, H <= 2^20 (the bound above), so all four taps read the centre texel
+        // tM.  Then a = (s + s) * 0.5 = s and b = s * 0.5 + (s + s) * 0.25 = s
+        // exactly, luma(b) = lM lies in [lMin, lMax], c = s, and unorm8 of
+        // byte / 255 is the byte again for all 256 bytes: the output is tM.
+        // Taken when a whole row of the wave is short-span (smooth regions).
+        if (__builtin_amdgcn_ballot_w64(fmaxf(fabsf(dxs), fabsf(dys)) > 0.5f) == 0) return tM;
+#endif
+        dx = dxs * ivx;
+        dy = dys * ivy;
         RGB s1 = span_tap(fx + dx * k1, fy + dy * k1);
         RGB s2 = span_tap(fx + dx * k2, fy + dy * k2);
         RGB a = RGB{(s1.r + s2.r) * 0.5f, (s1.g + s2.g) * 0.5f, (s1.b + s2.b) * 0.5f};
