@@ -128,6 +128,9 @@ __global__ __launch_bounds__(256) void rm_fxaa_kernel(const uint32_t* __restrict
 #ifndef RM_FXAA_FLAT
 #define RM_FXAA_FLAT 1  // short-span rows output their centre texel (below)
 #endif
+#ifndef RM_FXAA_BW
+#define RM_FXAA_BW 8  // a wave pass covers BW x (64 / BW) pixels: 8x8 blocks (64: one row)
+#endif
 // RM_FXAA_HALO: the span texels lie within +-4 of the pixel (above), so a
 // halo of 4 holds them all; RM_FXAA_TRIM: lumas only for the texels the +-1
 // taps read, (TX + 2) x (TY + 2), not the whole block; RM_FXAA_NW: waves per
@@ -257,8 +260,10 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
     const float FXAA_REDUCE_MIN = 1.0f / 128.0f, FXAA_REDUCE_MUL = 1.0f / 8.0f, FXAA_SPAN_MAX = 8.0f;
     const float ivx = 1.0f / (float)W, ivy = 1.0f / (float)H;  // inverseVP = 1 / u_resolution
     const float k1 = 1.0f / 3.0f - 0.5f, k2 = 2.0f / 3.0f - 0.5f;
-    const int x = x0 + lane;
-    const float fx = ((float)x + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
+    constexpr int BW = RM_FXAA_BW, BH = 64 / BW, NBX = FXL_TX / BW;
+    static_assert(BW * BH == 64 && FXL_TX % BW == 0 && FXL_TY % BH == 0, "RM_FXAA_BW: blocks tile the tile");
+    const int xl = x0 + lane;
+    const float fx_lane = ((float)xl + 0.5f) / (float)W;  // post.frag:140: uv = (tc.x, 1 - tc.y)
     // a span tap: post.frag's float address (NEAREST), then the staged texel
     // (block row * FXL_W as a 24-bit multiply: the row is clamped into the block)
 #if RM_FXAA_GTAP
@@ -299,11 +304,15 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
     const float fy_lane = 1.0f - ((float)min(y0 + (lane & (FXL_TY - 1)), H - 1) + 0.5f) / (float)H;
     // one pixel of row y0 + ly (its value; rows past the frame are computed on a
     // clamped row and not stored)
-    auto pixel = [&](int ly) -> uint32_t {
+    // pixel block b of the tile: lane -> column col, row ly (BW = 64: row b)
+    auto px_col = [&](int b) { return (b % NBX) * BW + (BW == 64 ? lane : (lane & (BW - 1))); };
+    auto px_row = [&](int b) { return (b / NBX) * BH + (BW == 64 ? 0 : lane / BW); };
+    auto pixel = [&](int blk) -> uint32_t {
+        const int col = px_col(blk), ly = px_row(blk);
         const int y = min(y0 + ly, H - 1);
         const int rr = FXL_TY - 1 - (y - y0);  // block row of the pixel's texel, less the halo
-        const int m = (rr + FXL_HALO) * FXL_W + (lane + FXL_HALO);
-        const int ml = (rr + FXL_HALO - SL_O) * SL_W + (lane + FXL_HALO - SL_O);
+        const int m = (rr + FXL_HALO) * FXL_W + (col + FXL_HALO);
+        const int ml = (rr + FXL_HALO - SL_O) * SL_W + (col + FXL_HALO - SL_O);
 #if RM_FXAA_F4
         const float lNW = sf4[m - FXL_W - 1].w, lNE = sf4[m - FXL_W + 1].w, lSW = sf4[m + FXL_W - 1].w;
         const float lSE = sf4[m + FXL_W + 1].w, lM = sf4[m].w;
@@ -312,12 +321,19 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
         const float lNW = slum[ml - SL_W - 1], lNE = slum[ml - SL_W + 1], lSW = slum[ml + SL_W - 1];
         const float lSE = slum[ml + SL_W + 1], lM = slum[ml];
 #if RM_FXAA_GTAP
-        const uint32_t tM = in[(size_t)(H - 1 - y) * W + (x < W ? x : W - 1)];  // (the centre texel, stex[m])
+        const uint32_t tM = in[(size_t)(H - 1 - y) * W + min(x0 + col, W - 1)];  // (the centre texel, stex[m])
 #else
         const uint32_t tM = stex[m];
 #endif
 #endif
-        const float fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_lane), ly));
+        float fx, fy;
+        if constexpr (BW == 64) {
+            fx = fx_lane;
+            fy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_lane), ly));
+        } else {  // (lane col's fx and lane ly's fy, one ds_bpermute each)
+            fx = __int_as_float(__builtin_amdgcn_ds_bpermute(col * 4, __float_as_int(fx_lane)));
+            fy = __int_as_float(__builtin_amdgcn_ds_bpermute(ly * 4, __float_as_int(fy_lane)));
+        }
         // (lumas are never NaN or -0: IEEE minimum/maximum, v_minimum3/v_maximum3,
         // equal GLSL min/max here without minNum's canonicalizing v_max per operand)
         const float lMin = __builtin_elementwise_minimum(
@@ -352,7 +368,7 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
         // tM.  Then a = (s + s) * 0.5 = s and b = s * 0.5 + (s + s) * 0.25 = s
         // exactly, luma(b) = lM lies in [lMin, lMax], c = s, and unorm8 of
         // byte / 255 is the byte again for all 256 bytes: the output is tM.
-        // Taken when a whole row of the wave is short-span (smooth regions).
+        // Taken when the wave's whole row (or block, RM_FXAA_BW) is short-span.
         if (__builtin_amdgcn_ballot_w64(fmaxf(fabsf(dxs), fabsf(dys)) > 0.5f) == 0) return tM;
 #endif
         dx = dxs * ivx;
@@ -374,6 +390,8 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
     // -> span taps) interleave
 #if RM_FXAA_ROWS == 4
     constexpr int N = FXL_NW;
+    static_assert(BW == 64, "RM_FXAA_ROWS = 4: row passes");
+    const int x = xl;
     for (int ly = wv; ly < FXL_TY; ly += 4 * N) {
         const uint32_t v0 = pixel(ly), v1 = pixel(ly + N), v2 = pixel(ly + 2 * N), v3 = pixel(ly + 3 * N);
         if (x < W && y0 + ly < H) out[(size_t)(y0 + ly) * W + x] = v0;
@@ -382,10 +400,12 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
         if (x < W && y0 + ly + 3 * N < H) out[(size_t)(y0 + ly + 3 * N) * W + x] = v3;
     }
 #else
-    for (int ly = wv; ly < FXL_TY; ly += 2 * FXL_NW) {
-        const uint32_t v0 = pixel(ly), v1 = pixel(ly + FXL_NW);
-        if (x < W && y0 + ly < H) out[(size_t)(y0 + ly) * W + x] = v0;
-        if (x < W && y0 + ly + FXL_NW < H) out[(size_t)(y0 + ly + FXL_NW) * W + x] = v1;
+    constexpr int NB = (FXL_TX / BW) * (FXL_TY / BH);  // pixel blocks (rows when BW = 64) per tile
+    for (int b = wv; b < NB; b += 2 * FXL_NW) {
+        const uint32_t v0 = pixel(b), v1 = pixel(b + FXL_NW);
+        const int xa = x0 + px_col(b), ya = y0 + px_row(b), xb = x0 + px_col(b + FXL_NW), yb = y0 + px_row(b + FXL_NW);
+        if (xa < W && ya < H) out[(size_t)ya * W + xa] = v0;
+        if (xb < W && yb < H) out[(size_t)yb * W + xb] = v1;
     }
 #endif
 }
