@@ -17,7 +17,8 @@
 //
 // Rows whose span is short output their centre texel without the span taps
 // (RM_FXAA_FLAT, proof at the test): 0.069-0.072 -> 0.052-0.053 ms on the C3
-// frame, same bits (profiles/r05/fxaa_flat/).
+// frame, same bits (profiles/r05/fxaa_flat/); with 8x8-pixel blocks per wave
+// pass (RM_FXAA_BW) instead of rows, 0.046-0.047 (profiles/r05/fxaa_blocks/).
 // Its own translation unit (split from rm_post.hip in round 5) so that it can
 // be scheduled with LLVM's max-ilp strategy, which shortens the latency-bound
 // FXAA kernel (0.0721-0.0729 -> 0.0697-0.0706 ms) but slows bloom's
