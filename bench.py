@@ -91,6 +91,8 @@ def parse():
     ap.add_argument("--walk-speed", type=float, default=0.1, help="camera step per frame (main.cpp:21 speed)")
     ap.add_argument("--walk-dt", type=float, default=1.0 / 60.0, help="u_time step per frame (main.cpp:30)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--post-pmc", default=os.path.join(HERE, "profiles", "pmc_post.json"),
+                    help="per post pass rocprofv3 HBM bytes (tools/make_post_traffic.py)")
     ap.add_argument("--pmc", default=os.path.join(HERE, "profiles", "pmc_counters.json"),
                     help="per-workload rocprofv3 PMC counters (profiles/): executed FP32 ops for "
                          "roofline.achieved, HBM bytes for roofline.traffic, VALU/SALU issue")
@@ -205,24 +207,123 @@ def _median(xs):
     return xs[len(xs) // 2]
 
 
-def time_fxaa(r, frame8, stream, reps=20):
+def post_plan(W, H):
+    """bloom's level pair and passes as rm_post.hip's bloom_plan computes them
+    (lod = log2(0.05 H) in float32, levels d1 = floor(lod), d2 = d1 + 1), and
+    which mip path a W x H frame takes: the exact-halving pyramid from level
+    s0 (W, H multiples of 2^d2, 5..8 levels), per-level resamples otherwise;
+    chain: rm_post_chain's fused path (the FXAA kernel writes level 3 and the
+    pyramid starts there: d2 - 3 in [5, 8], W, H multiples of 2^d2 and of the
+    FXAA tile 64 x 32, W, H <= 2^20)."""
+    import numpy as np
+
+    q = max(W, H).bit_length() - 1
+    lod = float(np.log2(np.float32(0.05) * np.float32(H)))
+    d1 = d2 = 0
+    if lod > 0:
+        d1 = min(int(np.floor(lod)), q)
+        d2 = min(d1 + 1, q)
+    w, h = [W], [H]
+    for _ in range(d2):
+        w.append(max(w[-1] >> 1, 1))
+        h.append(max(h[-1] >> 1, 1))
+    T2 = 1 << d2
+    div = W % T2 == 0 and H % T2 == 0
+    s0 = max(d2 - 8, 0)
+    pyramid = lod > 0 and d2 - s0 >= 5 and div
+    chain = (lod > 0 and 5 <= d2 - 3 <= 8 and div and W % 64 == 0 and H % 32 == 0 and W <= 1 << 20
+             and H <= 1 << 20)
+    nruns = [min(n, 5 * lw + 1) for n, lw in ((W, w[d1]), (H, h[d1]), (W, w[d2]), (H, h[d2]))] if lod > 0 else []
+    return dict(lod=lod, d1=d1, d2=d2, w=w, h=h, s0=s0, pyramid=pyramid, chain=chain, nruns=nruns)
+
+
+def post_bytes(W, H, which):
+    """Algorithmic HBM bytes of one post pass over a W x H RGBA8 frame, per
+    kernel: what each kernel must read and write once (re-reads served by the
+    caches not counted).  which: "fxaa" (rm_fxaa), "bloom" (rm_bloom of a
+    frame), "chain" (rm_post_chain: FXAA then bloom of its output).
+      fxaa       the frame in, the frame out (4 + 4 B/px); in the chain also
+                 mip level 3 out (4 B per 8 x 8 block)
+      mips       the level the pyramid starts from in (the frame: s0 = 0;
+                 level 3 in the chain), levels d1 and d2 out; without the
+                 pyramid every level 1..d2 out and its parent in
+      poly       levels d1, d2 in, the run-pair polynomials out (48 B a pair)
+      bloom_min  the frame in and out, the polynomials and the per-column /
+                 per-row run entries (24 B each) in
+    The run tables (rm_bloom_runs_kernel) depend on W x H only and are built
+    once per size, outside the per-frame bytes."""
+    P = post_plan(W, H)
+    px = 4 * W * H
+    k = {}
+    if which in ("fxaa", "chain"):
+        k["fxaa"] = 2 * px + (px // 64 if which == "chain" and P["chain"] else 0)
+    if which == "fxaa":
+        return dict(kernels=k, total=sum(k.values()), plan=P)
+    if P["lod"] <= 0:
+        k["bloom"] = 2 * px
+        return dict(kernels=k, total=sum(k.values()), plan=P)
+    w, h, d1, d2 = P["w"], P["h"], P["d1"], P["d2"]
+    lv = lambda j: 4 * w[j] * h[j]  # noqa: E731
+    if which == "chain" and P["chain"]:
+        k["mips"] = lv(3) + lv(d1) + lv(d2)
+    elif P["pyramid"]:
+        s0 = P["s0"]
+        k["mips"] = sum(lv(j - 1) + lv(j) for j in range(1, s0 + 1)) + lv(s0) + lv(d1) + lv(d2)
+    else:
+        k["mips"] = sum(lv(j - 1) + lv(j) for j in range(1, d2 + 1))
+    nr = P["nruns"]
+    tabs = 48 * (nr[0] * nr[1] + nr[2] * nr[3])
+    k["poly"] = lv(d1) + lv(d2) + tabs
+    k["bloom_min"] = 2 * px + tabs + 24 * (W + H)
+    return dict(kernels=k, total=sum(k.values()), plan=P)
+
+
+def load_post_counters(path):
+    """profiles/pmc_post.json (tools/make_post_traffic.py): per post pass and
+    frame size, the rocprofv3 HBM bytes of one pass, (2 FETCH_SIZE +
+    WRITE_SIZE) per kernel launch summed over the pass's kernels."""
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+
+
+def _post_line(name, ms, W, H, which, counters):
+    b = post_bytes(W, H, which)
+    gbs = b["total"] / (ms / 1e3) / 1e9
+    line = {"name": name, "ms": ms, "bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": b["total"], "algorithmic_bytes_per_kernel": b["kernels"],
+            "traffic": None, "counter_frac": None}
+    c = counters.get(f"{which}_{W}x{H}")
+    if c:
+        line.update(traffic=c["hbm_bytes"], counter_frac=c["hbm_bytes"] / (ms / 1e3) / 1e9 / PEAK_HBM_GBS,
+                    traffic_per_kernel=c.get("kernels"), traffic_source=c.get("source"),
+                    traffic_note="rocprofv3 (2 FETCH_SIZE + WRITE_SIZE) per pass, profiles/pmc_post.json")
+    return line
+
+
+def _timed(stream, reps, fn):
+    import torch
+
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def time_fxaa(r, frame8, stream, counters, reps=20):
     """The reference's FXAA pass (post.frag) over the RGBA8 frame on rank 0:
     HBM-bound stencil, 4 B read + 4 B written per pixel (algorithmic)."""
     import torch
 
+    H, W = frame8.shape
     out = torch.empty_like(frame8)
-    r.fxaa(frame8, out=out)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(reps):
-        r.fxaa(frame8, out=out)
-    e1.record(stream)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    nbytes = frame8.numel() * 8
-    gbs = nbytes / (ms / 1e3) / 1e9
-    return {"name": "fxaa (post.frag:16-61,135-144)", "ms": ms, "bound": "hbm", "achieved": gbs,
-            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": nbytes}
+    ms = _timed(stream, reps, lambda: r.fxaa(frame8, out=out))
+    return _post_line("fxaa (post.frag:16-61,135-144)", ms, W, H, "fxaa", counters)
 
 
 # per pixel (rm_post.hip rm_bloom_min_kernel): the base-level bilinear fetch
@@ -232,37 +333,58 @@ def time_fxaa(r, frame8, stream, reps=20):
 BLOOM_FLOP_PER_PX = 27 + 2 * 3 * 3 * 2 + 3 + 9
 
 
-def time_bloom(r, frame8, stream, reps=20):
+def time_bloom(r, frame8, stream, counters, reps=20):
     """The reference's bloom pass (bloom.frag + its mip chain, main.cpp:212-214)
-    over the RGBA8 frame on rank 0.  Its roofline is HBM: the frame read twice
-    (mip level 1, the base-level fetch) and written once, mip levels 1..d2
-    written and read once (algorithmic bytes); per pixel two bilinear
-    polynomials (BLOOM_FLOP_PER_PX) are reported beside it."""
-    import math
-
+    over an RGBA8 frame on rank 0, priced by the bytes its kernels move
+    (post_bytes "bloom"); per pixel two bilinear polynomials
+    (BLOOM_FLOP_PER_PX) are reported beside it."""
     import torch
 
     H, W = frame8.shape
     out = torch.empty_like(frame8)
-    r.bloom(frame8, out=out)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(reps):
-        r.bloom(frame8, out=out)
-    e1.record(stream)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    lod = math.log2(0.05 * H)
-    d2 = min(int(math.floor(lod)) + 1, int(math.log2(max(W, H)))) if lod > 0 else 0
-    mip_texels = sum(max(1, W >> k) * max(1, H >> k) for k in range(1, d2 + 1))
-    nbytes = 4 * (3 * W * H + 2 * mip_texels)
-    gbs = nbytes / (ms / 1e3) / 1e9
+    ms = _timed(stream, reps, lambda: r.bloom(frame8, out=out))
+    line = _post_line("bloom (shaders/post/bloom.frag:14-43 + mip chain)", ms, W, H, "bloom", counters)
     tflops = W * H * BLOOM_FLOP_PER_PX / (ms / 1e3) / 1e12
-    return {"name": "bloom (shaders/post/bloom.frag:14-43 + mip chain)", "ms": ms, "bound": "hbm",
-            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-            "algorithmic_bytes": nbytes, "mip_levels": d2,
-            "valu": {"flop_per_px": BLOOM_FLOP_PER_PX, "achieved": tflops, "peak": PEAK_FP32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": tflops / PEAK_FP32_TFLOPS}}
+    line.update(mip_levels=post_plan(W, H)["d2"],
+                valu={"flop_per_px": BLOOM_FLOP_PER_PX, "achieved": tflops, "peak": PEAK_FP32_TFLOPS,
+                      "unit": "TFLOP/s", "frac": tflops / PEAK_FP32_TFLOPS})
+    return line
+
+
+def time_pipeline(r, W, H, stream, counters, render_ms, reps=20):
+    """The reference's whole frame (main.cpp:196-214) on rank 0: the ray-march
+    pass into the RGBA8 frame, FXAA into postTexture, its mip chain and bloom of
+    it into the output (rm_post_chain), frame after frame on one stream.
+    pipeline_ms = event interval per frame; post_chain = the two post passes
+    alone; chain_check: rm_post_chain's output against rm_fxaa then rm_bloom of
+    the same frame (GPU, bit for bit; tests/test_post_chain.py holds the
+    oracle's chain)."""
+    import torch
+
+    frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    mid, out = torch.empty_like(frame), torch.empty_like(frame)
+
+    def step():
+        r.render_rgba8(W, H, out=frame)
+        r.post_chain(frame, mid=mid, out=out)
+
+    for _ in range(3):
+        step()
+    pipe_ms = _timed(stream, reps, step)
+    chain_ms = _timed(stream, reps, lambda: r.post_chain(frame, mid=mid, out=out))
+    ref = r.bloom(r.fxaa(frame))
+    torch.cuda.synchronize()
+    nd = int((ref != out).sum())
+    chain = _post_line("post chain: fxaa + mips + bloom (main.cpp:209-214, rm_post_chain)", chain_ms, W, H, "chain",
+                       counters)
+    chain["fused_level3"] = post_plan(W, H)["chain"]
+    return {"pipeline_ms": pipe_ms, "pipeline_frames_per_s": 1e3 / pipe_ms,
+            "render_ms": render_ms, "post_chain": chain,
+            "chain_check": {"result": "bit-exact" if nd == 0 else "MISMATCH", "pixels_differing": nd,
+                            "against": "rm_fxaa then rm_bloom of the last frame"},
+            "note": "render (adaptive order, as the timed frames) -> FXAA -> mip chain -> bloom of the FXAA frame, "
+                    f"{reps} frames back to back on one stream, HIP events around them; render_ms = the timed "
+                    "frames' ms_per_step"}
 
 
 def balanced_runs(world, band, H, ex):
@@ -639,7 +761,9 @@ def main():
         # by its own executed ray-steps; every rank's beside it
         crit = max(range(len(rank_launch)), key=lambda q: rank_launch[q]["kernel_ms"])
         cl = rank_launch[crit]
-        roof = roofline(pmc, cl["kernel_ms"], cl["executed_steps"],
+        ms_step = elapsed / args.steps * 1e3
+        # the roofline's launch duration: the median synchronous launch, never longer than the driver-timed step
+        roof = roofline(pmc, min(cl["kernel_ms"], ms_step), cl["executed_steps"],
                         W * cl["rows"] * (4 if args.fmt == "rgba8" else 16), flop_rank if crit == 0 else None,
                         evals_rank if crit == 0 else None, exact=exact, rows_frac=cl["rows"] / H)
         if world > 1:
@@ -698,8 +822,12 @@ def main():
         if exchange is not None:
             res.update(exchange)
         if fr.frame is not None and fr.fmt == "rgba8":
-            res["post_pass"] = time_fxaa(r, fr.frame, stream)
-            res["bloom_pass"] = time_bloom(r, fr.frame, stream)
+            counters = load_post_counters(args.post_pmc)
+            res["post_pass"] = time_fxaa(r, fr.frame, stream, counters)
+            res["bloom_pass"] = time_bloom(r, fr.frame, stream, counters)
+            if world == 1:
+                res["pipeline"] = time_pipeline(r, W, H, stream, counters, res["ms_per_step"])
+                res["pipeline_ms"] = res["pipeline"]["pipeline_ms"]
         if world == 1 and args.cpu_seconds > 0:
             res["cpu_baseline"] = cpu_baseline(args, pose, W, H, args.cpu_seconds)
         print(json.dumps(res), flush=True)

@@ -289,6 +289,18 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
  * stream changes. */
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
 
+/* The reference's two post passes of a frame, chained as main.cpp:209-214 runs
+ * them: FXAA of `in` into `mid` (post_shader into postTexture), then bloom of
+ * `mid` into `out` (postTexture.generateMipmap, post_bloom.apply).  The same
+ * bits as rm_fxaa(in -> mid) followed by rm_bloom(mid -> out); where the frame
+ * allows (W, H multiples of 2^d2 with bloom's levels d2 - 3 in [5, 8], e.g.
+ * 4096 x 4096, and of the FXAA kernel's 64 x 32 tile) the FXAA kernel also
+ * writes mip level 3 of `mid` from registers and the mip pyramid starts there
+ * instead of re-reading `mid`.  Device buffers of W x H RGBA8
+ * words, pairwise distinct, W*H < 2^30; asynchronous on the context's stream;
+ * bloom's scratch as rm_bloom's. */
+rm_status rm_post_chain(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *mid, uint32_t *out);
+
 /* ---- Weighted row parts: frame row y belongs to a part iff (y mod cycle) - offset
  * lies in [0, run).  Round-robin bands are the special case run = band,
  * cycle = band * nshards, offset = band * shard; parts with different runs give

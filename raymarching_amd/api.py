@@ -356,6 +356,20 @@ class Renderer:
         check(lib().rm_bloom(self._ctx, W, H, self._ptr(frame8), self._ptr(out)), self._ctx)
         return out
 
+    def post_chain(self, frame8, mid=None, out=None):
+        """main.cpp:209-214's post passes of a frame: FXAA of frame8 into mid,
+        then bloom of mid into out (rm_post_chain); returns (mid, out)."""
+        torch = _torch()
+        H, W = frame8.shape
+        if mid is None:
+            mid = torch.empty_like(frame8)
+        if out is None:
+            out = torch.empty_like(frame8)
+        for t in (frame8, mid, out):
+            _check_out(t, H * W)
+        check(lib().rm_post_chain(self._ctx, W, H, self._ptr(frame8), self._ptr(mid), self._ptr(out)), self._ctx)
+        return mid, out
+
     def scene_eval(self, points, material: bool = False):
         """sceneSDF(p) of the loaded scene at points [n, 3] (host, numpy):
         dist [n], and with material=True also the [n, 16] Material floats."""

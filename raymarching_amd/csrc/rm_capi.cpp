@@ -1259,6 +1259,28 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) 
     return mark_done(ctx);
 }
 
+// bloom's scratch (mip levels, run tables, polynomials) for W x H; whether its
+// run tables can be reused (the last bloom of this context had the same size
+// and stream: same buffer)
+static rm_status bloom_scratch(rm_ctx *ctx, const rm::BloomPlan &plan, int W, int H, bool &cached) {
+    if (plan.texels > ctx->mips_texels) {
+        if (ctx->mips) RM_HIP(hipFree(ctx->mips));
+        ctx->mips = nullptr;
+        ctx->mips_texels = 0;
+        ctx->bloom_runs_w = 0;
+        RM_HIP(hipMalloc(&ctx->mips, plan.texels * sizeof(uint32_t)));
+        ctx->mips_texels = plan.texels;
+    }
+    cached = ctx->bloom_runs_w == W && ctx->bloom_runs_h == H && ctx->bloom_runs_stream == ctx->stream;
+    ctx->bloom_runs_w = 0;
+    return RM_OK;
+}
+static void bloom_done(rm_ctx *ctx, int W, int H) {
+    ctx->bloom_runs_w = W;
+    ctx->bloom_runs_h = H;
+    ctx->bloom_runs_stream = ctx->stream;
+}
+
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     if (!in || !out || W <= 0 || H <= 0 || in == out)
@@ -1268,23 +1290,35 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
     RM_HIP(hipSetDevice(ctx->device));
     rm::TraceRange range("rm_bloom");
     const rm::BloomPlan plan = rm::bloom_plan(W, H);
-    if (plan.texels > ctx->mips_texels) {
-        if (ctx->mips) RM_HIP(hipFree(ctx->mips));
-        ctx->mips = nullptr;
-        ctx->mips_texels = 0;
-        ctx->bloom_runs_w = 0;
-        RM_HIP(hipMalloc(&ctx->mips, plan.texels * sizeof(uint32_t)));
-        ctx->mips_texels = plan.texels;
-    }
-    // the run tables depend on W x H only; reused when the last bloom of this
-    // context had the same size and stream (same buffer)
-    const bool cached = ctx->bloom_runs_w == W && ctx->bloom_runs_h == H && ctx->bloom_runs_stream == ctx->stream;
-    ctx->bloom_runs_w = 0;
+    bool cached = false;
+    if (rm_status st = bloom_scratch(ctx, plan, W, H, cached)) return st;
     hipError_t e = rm::launch_bloom(in, out, ctx->mips, plan, ctx->stream, cached);
     if (e != hipSuccess) return hip_fail(ctx, e, "bloom launch");
-    ctx->bloom_runs_w = W;
-    ctx->bloom_runs_h = H;
-    ctx->bloom_runs_stream = ctx->stream;
+    bloom_done(ctx, W, H);
+    return mark_done(ctx);
+}
+
+rm_status rm_post_chain(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *mid, uint32_t *out) {
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!in || !mid || !out || W <= 0 || H <= 0 || in == mid || mid == out || in == out)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_post_chain: bad arguments");
+    if ((int64_t)W * H >= ((int64_t)1 << 30))  // the FXAA kernel's 32-bit byte offsets
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_post_chain: frame of 2^30 texels or more");
+    if (!is_device_ptr(in) || !is_device_ptr(mid) || !is_device_ptr(out))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_post_chain: device pointers required");
+    RM_HIP(hipSetDevice(ctx->device));
+    rm::TraceRange range("rm_post_chain");
+    const rm::BloomPlan plan = rm::bloom_plan(W, H);
+    bool cached = false;
+    if (rm_status st = bloom_scratch(ctx, plan, W, H, cached)) return st;
+    // main.cpp:209-214: FXAA into postTexture, its mip chain, bloom of it; with
+    // plan.chain the FXAA kernel also writes mip level 3 and the pyramid starts
+    // there (no re-read of the FXAA frame for the mips)
+    hipError_t e = rm::launch_fxaa(in, mid, W, H, ctx->stream, plan.chain ? ctx->mips + plan.offset[3] : nullptr);
+    if (e != hipSuccess) return hip_fail(ctx, e, "post chain: fxaa launch");
+    e = rm::launch_bloom(mid, out, ctx->mips, plan, ctx->stream, cached, plan.chain);
+    if (e != hipSuccess) return hip_fail(ctx, e, "post chain: bloom launch");
+    bloom_done(ctx, W, H);
     return mark_done(ctx);
 }
 

@@ -48,7 +48,10 @@ hipError_t launch_deinterleave_cycle_rgb8(const uint8_t* gathered, uint32_t* out
 // for the following launch
 hipError_t launch_tile_order(const uint32_t* cost, int n, int gx, int radius, uint32_t* order, uint32_t* hist,
                              uint32_t* next, uint8_t* bucket, hipStream_t s);
-hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
+// l3 (optional): FXAA's output also as mip level 3 (W/8 x H/8 exact-halving
+// texels, see BloomPlan::chain); only where chain_fxaa_ok(W, H)
+hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s, uint32_t* l3 = nullptr);
+bool chain_fxaa_ok(int W, int H);
 // rm_wire.hip: the compressed RGB wire of RGBA8 row parts
 long long wire_capacity(int W, int n);
 long long wire_workspace(int W, int n);
@@ -82,11 +85,18 @@ struct BloomPlan {
     // polynomials (rm_post.hip).  All but the polynomials depend on W x H only.
     size_t base_ent[2] = {}, run_ent[4] = {}, run_tup[4] = {}, run_count = 0, poly_tab[2] = {};
     int nruns[4] = {};  // most runs an axis can have
+    // rm_post_chain (FXAA then bloom of its output): the FXAA kernel writes mip
+    // level 3 of its output from registers (8x8-pixel blocks, mip_mean4 chain)
+    // and the pyramid starts there, instead of re-reading the frame: set when
+    // levels 4..d2 are 5 to 8 exact halvings of level 3 (launch_bloom's
+    // pyramid kernel) and the FXAA kernel's blocks tile the frame
+    bool chain = false;
 };
 BloomPlan bloom_plan(int W, int H);
 // runs_cached: the buffer already holds this W x H's run tables, written on
 // this stream (only the mip levels and the polynomials are rebuilt)
+// from_l3 (p.chain): mips + p.offset[3] already holds level 3 of `in`
 hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s,
-                        bool runs_cached);
+                        bool runs_cached, bool from_l3 = false);
 
 }  // namespace rm

@@ -44,18 +44,7 @@ __global__ __launch_bounds__(256) void rm_mip_down_kernel(const uint32_t* __rest
     out[(size_t)y * w1 + x] = r;
 }
 
-// Exact halvings (even level sizes): rm_mip_down_kernel at sx = sy = 2 has
-// u = 2x + 0.5, a = b = 0.5 exactly and every float operation exact, so a
-// texel of the next level is the mean of its 2x2 texels rounded half to even,
-// per channel: (s + 1 + ((s >> 2) & 1)) >> 2 for the 4-texel sum s (s = 4q + r:
-// r < 2 -> q, r > 2 -> q + 1, r = 2 -> the even one of q, q + 1).  Two
-// channels per 32-bit add (16-bit fields, sums <= 1020).
-__device__ __forceinline__ uint32_t mip_mean4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    const uint32_t m = 0x00FF00FFu, one = 0x00010001u;
-    const uint32_t lo = (a & m) + (b & m) + (c & m) + (d & m);
-    const uint32_t hi = ((a >> 8) & m) + ((b >> 8) & m) + ((c >> 8) & m) + ((d >> 8) & m);
-    return (((lo + one + ((lo >> 2) & one)) >> 2) & m) | ((((hi + one + ((hi >> 2) & one)) >> 2) & m) << 8);
-}
+// Exact halvings (even level sizes): mip_mean4 (rm_post_common.h).
 
 // The mip levels below `src` (sw texels wide) by exact halvings, 2^(lgB + 5)
 // levels' worth of one src tile per workgroup: 1024 lanes, each reducing a
@@ -488,6 +477,8 @@ BloomPlan bloom_plan(int W, int H) {
         p.d2 = p.d1 + 1 > q ? q : p.d1 + 1;
     }
     p.fr = p.lod - floorf(p.lod);
+    const long long T2c = 1LL << (p.d2 < 62 ? p.d2 : 62);
+    p.chain = p.lod > 0.0f && p.d2 - 3 >= 5 && p.d2 - 3 <= 8 && W % T2c == 0 && H % T2c == 0 && chain_fxaa_ok(W, H);
     int w = W, h = H;
     p.w[0] = W;
     p.h[0] = H;
@@ -529,18 +520,22 @@ BloomPlan bloom_plan(int W, int H) {
 }
 
 hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s,
-                        bool runs_cached) {
+                        bool runs_cached, bool from_l3) {
     const int W = p.w[0], H = p.h[0];
     if (W <= 0 || H <= 0) return hipSuccess;
+    if (from_l3 && !p.chain) return hipErrorInvalidValue;
     const uint32_t* lv[40] = {in};
     // levels 1..d2: when W and H are multiples of 2^d2 every level is an exact
     // halving, and the last 5..8 levels come from one rm_mip_pyramid_kernel
     // launch over level s = max(d2 - 8, 0) (only d1, d2 written); otherwise,
     // and for levels 1..s, one rm_mip_down_kernel launch per level
+    // (from_l3: level 3 is in the buffer, written by the FXAA kernel of rm_post_chain, and the pyramid
+    // starts there)
     const long long T2 = 1LL << (p.d2 < 62 ? p.d2 : 62);
-    const int s0 = p.d2 > 8 ? p.d2 - 8 : 0;
+    const int s0 = from_l3 ? 3 : p.d2 > 8 ? p.d2 - 8 : 0;
     const bool pyramid = p.lod > 0.0f && p.d2 - s0 >= 5 && W % T2 == 0 && H % T2 == 0;
-    for (int k = 1; k <= (pyramid ? s0 : p.d2); k++) {
+    if (from_l3) lv[3] = mips + p.offset[3];
+    for (int k = from_l3 ? 4 : 1; k <= (pyramid ? s0 : p.d2); k++) {
         uint32_t* dst = mips + p.offset[k];
         const int w = p.w[k - 1], h = p.h[k - 1], w1 = p.w[k], h1 = p.h[k];
         hipLaunchKernelGGL(rm_mip_down_kernel, dim3((w1 + 15) / 16, (h1 + 15) / 16), dim3(256), 0, s, lv[k - 1], dst,

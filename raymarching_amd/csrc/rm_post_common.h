@@ -50,4 +50,19 @@ __device__ __forceinline__ uint32_t unorm8_finite(float c) {
     return (uint32_t)__float2int_rn(__builtin_amdgcn_fmed3f(c, 0.0f, 1.0f) * 255.0f);
 }
 
+// One texel of the next mip level by an exact halving (even level sizes): the
+// bilinear resample of glGenerateMipmap at sx = sy = 2 has u = 2x + 0.5, a = b
+// = 0.5 exactly and every float operation exact, so the texel is the mean of
+// its 2x2 texels rounded half to even, per channel: (s + 1 + ((s >> 2) & 1))
+// >> 2 for the 4-texel sum s (s = 4q + r: r < 2 -> q, r > 2 -> q + 1, r = 2 ->
+// the even one of q, q + 1).  Two channels per 32-bit add (16-bit fields, sums
+// <= 1020).  Used by bloom's mip pyramid (rm_post.hip) and by FXAA's level-3
+// epilogue (rm_fxaa.hip, rm_post_chain).
+__device__ __forceinline__ uint32_t mip_mean4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint32_t m = 0x00FF00FFu, one = 0x00010001u;
+    const uint32_t lo = (a & m) + (b & m) + (c & m) + (d & m);
+    const uint32_t hi = ((a >> 8) & m) + ((b >> 8) & m) + ((c >> 8) & m) + ((d >> 8) & m);
+    return (((lo + one + ((lo >> 2) & one)) >> 2) & m) | ((((hi + one + ((hi >> 2) & one)) >> 2) & m) << 8);
+}
+
 }  // namespace rm

@@ -118,3 +118,53 @@ def test_stale_counters_give_no_frac(scale):
     assert "valu_issue" not in r and "salu_issue" not in r
     ok = bench.roofline(C3, C3["avg_kernel_ns_trace"] / 1e6 * 1.05, C3["executed_ray_steps_per_launch"], 1, None, None)
     assert ok["frac"] is not None and ok["valu_issue"]["frac"] < 1
+
+
+# ---- post passes: algorithmic bytes against the counted bytes
+POST = json.load(open(os.path.join(ROOT, "profiles", "pmc_post.json")))
+
+
+def _post_key(key):
+    which, size = key.rsplit("_", 1)
+    W, H = (int(v) for v in size.split("x"))
+    return which, W, H
+
+
+def test_post_counters_present():
+    assert {"fxaa_4096x4096", "bloom_4096x4096"} <= set(POST)
+
+
+@pytest.mark.parametrize("key", sorted(POST))
+def test_post_bytes_within_counters(key):
+    """No post pass prices more bytes than its kernels move: each kernel's
+    algorithmic bytes (bench.post_bytes) and the pass's total stay within 10 %
+    of the rocprofv3 HBM bytes of the same kernels (2 FETCH + WRITE)."""
+    which, W, H = _post_key(key)
+    b = bench.post_bytes(W, H, which)
+    c = POST[key]
+    assert set(b["kernels"]) == set(c["kernels"]), (b["kernels"], c["kernels"])
+    for k, v in b["kernels"].items():
+        assert v <= 1.1 * c["kernels"][k], (key, k, v, c["kernels"][k])
+    assert b["total"] <= 1.1 * c["hbm_bytes"]
+
+
+def test_post_line_fracs_below_peak():
+    counters = {"bloom_4096x4096": POST["bloom_4096x4096"]}
+    line = bench._post_line("bloom", 0.05, 4096, 4096, "bloom", counters)
+    assert line["algorithmic_bytes"] == bench.post_bytes(4096, 4096, "bloom")["total"]
+    assert line["frac"] < 1 and line["counter_frac"] < 1
+    assert line["traffic"] == POST["bloom_4096x4096"]["hbm_bytes"]
+
+
+def test_post_bytes_model():
+    P = bench.post_plan(4096, 4096)
+    assert (P["d1"], P["d2"], P["pyramid"], P["chain"]) == (7, 8, True, True)
+    px = 4 * 4096 * 4096
+    bl, ch = bench.post_bytes(4096, 4096, "bloom"), bench.post_bytes(4096, 4096, "chain")
+    # bloom of a frame reads it twice (pyramid, base texel) and writes it once;
+    # the chain reads the FXAA frame once for bloom (the mips start at level 3)
+    assert 3 * px < bl["total"] < 3.05 * px
+    assert ch["kernels"]["mips"] < px / 50
+    assert ch["total"] < bench.post_bytes(4096, 4096, "fxaa")["total"] + bl["total"] - 0.9 * px
+    # lod <= 0: one kernel, frame in and out
+    assert bench.post_bytes(64, 16, "bloom")["kernels"] == {"bloom": 2 * 4 * 64 * 16}

@@ -30,5 +30,6 @@ if [ "${PMC:-0}" = 1 ]; then
   bash tools/pmc_profile.sh O8192$TAG --scene O --size 8192 --max-steps 512 || exit 9
   bash tools/pmc_post.sh fxaa && mv gpurun_out/pmc_fxaa $O/pmc_fxaa || exit 10
   bash tools/pmc_post.sh bloom && mv gpurun_out/pmc_bloom $O/pmc_bloom || exit 11
+  bash tools/pmc_post.sh post_chain && mv gpurun_out/pmc_post_chain $O/pmc_post_chain || exit 12
 fi
 echo "validate $TAG done"

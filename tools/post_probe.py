@@ -1,6 +1,7 @@
 """Post-pass driver for rocprofv3 runs: one 4096^2 scene-T RGBA8 frame, then
-`reps` passes of `fxaa` or `bloom` over it (tools/; not part of the product).
-Usage: post_probe.py fxaa|bloom [W] [H] [reps]"""
+`reps` passes of `fxaa`, `bloom` or `post_chain` (FXAA then bloom of its
+output, rm_post_chain) over it (tools/; not part of the product).
+Usage: post_probe.py fxaa|bloom|post_chain [W] [H] [reps]"""
 import os
 import sys
 
@@ -19,9 +20,12 @@ r.set_pose(*[rm.POSES["P0"][k] for k in ("pos", "mouse", "time")])
 r.set_params(max_steps=256, count_evals=0)
 frame = r.render_rgba8(W, H)
 out = torch.empty_like(frame)
-fn = getattr(r, which)
+mid = torch.empty_like(frame)
 for _ in range(reps):
-    fn(frame, out=out)
+    if which == "post_chain":
+        r.post_chain(frame, mid=mid, out=out)
+    else:
+        getattr(r, which)(frame, out=out)
 torch.cuda.synchronize()
 print("post probe done", which, W, H, reps)
 r.close()

@@ -24,6 +24,9 @@ __global__ __launch_bounds__(256) void k(float* out, float a, float b) {
     float x[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) x[j] = threadIdx.x * 1e-3f + j;
+    // VGPR operands that the compiler cannot fold into SGPRs
+    const float va = a + threadIdx.x * 1e-9f, vb = b + threadIdx.x * 1e-9f;
+    const f2 vp = f2{va, va}, vq = f2{vb, vb};
     f2 y[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) y[j] = f2{x[2 * j], x[2 * j + 1]};
@@ -40,6 +43,48 @@ __global__ __launch_bounds__(256) void k(float* out, float a, float b) {
         if constexpr (OP == 1) {
 #pragma unroll
             for (int j = 0; j < 4; j++) y[j] = __builtin_elementwise_fma(y[j], f2{a, a}, f2{b, b});  // v_pk_fma_f32
+        }
+        if constexpr (OP == 7) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) y[j] = y[j] + f2{a, b};  // v_pk_add_f32
+        }
+        if constexpr (OP == 8) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) y[j] = y[j] * f2{a, b};  // v_pk_mul_f32
+        }
+        if constexpr (OP == 10) {  // v_fma_f32, all VGPR operands
+#pragma unroll
+            for (int j = 0; j < 8; j++) x[j] = fmaf(x[j], va, vb);
+        }
+        if constexpr (OP == 11) {  // v_mul_f32, VGPR operand
+#pragma unroll
+            for (int j = 0; j < 8; j++) x[j] = x[j] * va;
+        }
+        if constexpr (OP == 12) {  // v_floor_f32
+#pragma unroll
+            for (int j = 0; j < 8; j++) x[j] = floorf(x[j]);
+        }
+        if constexpr (OP == 13) {  // v_add_f32 with an inline constant
+#pragma unroll
+            for (int j = 0; j < 8; j++) x[j] = x[j] + 1.0f;
+        }
+        if constexpr (OP == 14) {  // v_pk_fma_f32, VGPR operands
+#pragma unroll
+            for (int j = 0; j < 4; j++) y[j] = __builtin_elementwise_fma(y[j], vp, vq);
+        }
+        if constexpr (OP == 15) {  // v_fma_f32 with an inline constant and a VGPR
+#pragma unroll
+            for (int j = 0; j < 8; j++) x[j] = fmaf(x[j], va, 0.5f);
+        }
+        if constexpr (OP == 16) {  // v_max3_f32, VGPR operands
+#pragma unroll
+            for (int j = 0; j < 8; j++) x[j] = fmaxf(x[j], fmaxf(va, vb));
+        }
+        if constexpr (OP == 9) {  // 2 v_pk_fma_f32 + 4 v_fma_f32 interleaved
+#pragma unroll
+            for (int j = 0; j < 2; j++) y[j] = __builtin_elementwise_fma(y[j], f2{a, a}, f2{b, b});
+#pragma unroll
+            for (int j = 0; j < 4; j++) x[j] = fmaf(x[j], a, b);
         }
     }
     float s = 0;
@@ -77,7 +122,19 @@ int run(const char* name, int ops_per_iter) {
 int main() {
     run<0>("v_fma_f32 x8", 8);
     run<1>("v_pk_fma_f32 x4", 4);
+    run<7>("v_pk_add_f32 x4", 4);
+    run<8>("v_pk_mul_f32 x4", 4);
+    run<9>("2 v_pk_fma + 4 v_fma", 6);
+    run<0>("v_fma_f32 x8 (again)", 8);
+    run<1>("v_pk_fma_f32 x4 (again)", 4);
     run<5>("v_mul_f32 x8", 8);
+    run<10>("v_fma_f32 x8 (vgpr ops)", 8);
+    run<11>("v_mul_f32 x8 (vgpr op)", 8);
+    run<12>("v_floor_f32 x8", 8);
+    run<13>("v_add_f32 x8 (inline 1.0)", 8);
+    run<14>("v_pk_fma_f32 x4 (vgpr)", 4);
+    run<15>("v_fma_f32 x8 (vgpr, inl)", 8);
+    run<16>("v_max3_f32 x8 (vgpr)", 8);
     run<2>("v_mul+v_floor x8", 16);
     run<3>("v_med3_f32 x8", 8);
     run<6>("v_fract_f32 x8", 8);
