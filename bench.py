@@ -427,7 +427,19 @@ def pmc_flop(pmc):
 PMC_TIME_TOL = (0.9, 1.1)
 
 
-def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=True, rows_frac=1.0):
+def pmc_build_mismatch(pmc, code_hash):
+    """Why a PMC entry does not count this build's render launch, or None: its
+    render_code_hash (tools/make_traffic_json.py) differs from the loaded
+    library's rm_render_code_hash().  Entries without a hash (older profiles)
+    are checked by launch duration only (roofline)."""
+    h = pmc.get("render_code_hash") if pmc else None
+    if h and code_hash and h != code_hash:
+        return (f"the PMC counters in profiles/pmc_counters.json ({pmc.get('source')}) were taken with render code "
+                f"{h}, this library's is {code_hash}")
+    return None
+
+
+def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=True, rows_frac=1.0, code_hash=None):
     """The render kernel's FP32-VALU roofline for one launch of kern_ms that
     executed `executed_steps` ray-steps and wrote out_bytes.
 
@@ -446,8 +458,10 @@ def roofline(pmc, kern_ms, executed_steps, out_bytes, flop_tally, evals, exact=T
     t = kern_ms / 1e3
     cnt = pmc_flop(pmc) if pmc else None
     base_steps = pmc.get("executed_ray_steps_per_launch") if pmc else None
-    stale = None
-    if exact and pmc and pmc.get("avg_kernel_ns_trace"):
+    stale = pmc_build_mismatch(pmc, code_hash)  # (every path: exact, a rank's share, a walk)
+    if stale:
+        cnt = None
+    if not stale and exact and pmc and pmc.get("avg_kernel_ns_trace"):
         # counters of another build: the profiled launch's duration is off this one's by > 10 %
         ratio = kern_ms * 1e6 / pmc["avg_kernel_ns_trace"]
         if not PMC_TIME_TOL[0] <= ratio <= PMC_TIME_TOL[1]:
@@ -763,13 +777,16 @@ def main():
         cl = rank_launch[crit]
         ms_step = elapsed / args.steps * 1e3
         # the roofline's launch duration: the median synchronous launch, never longer than the driver-timed step
+        code_hash = rm.render_code_hash()
         roof = roofline(pmc, min(cl["kernel_ms"], ms_step), cl["executed_steps"],
                         W * cl["rows"] * (4 if args.fmt == "rgba8" else 16), flop_rank if crit == 0 else None,
-                        evals_rank if crit == 0 else None, exact=exact, rows_frac=cl["rows"] / H)
+                        evals_rank if crit == 0 else None, exact=exact, rows_frac=cl["rows"] / H, code_hash=code_hash)
+        roof["render_code_hash"] = code_hash
         if world > 1:
             roof["rank"] = crit
             roof["per_rank_frac"] = [roofline(pmc, q["kernel_ms"], q["executed_steps"], 0, None, None, exact=False,
-                                              rows_frac=q["rows"] / H)["frac"] for q in rank_launch]
+                                              rows_frac=q["rows"] / H, code_hash=code_hash)["frac"]
+                                     for q in rank_launch]
         res = {
             "metric": "ray-steps/sec + frames/sec at 4096\u00d74096, 1/2/4/8 MI355X",
             "value": evals_frame * args.steps / elapsed,

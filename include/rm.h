@@ -286,7 +286,9 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
  * in/out: W x H device buffers, row 0 first, in != out.  Asynchronous on the
  * context's stream.  The scratch buffer also keeps the size's run tables
  *  between calls; they are rebuilt when W x H or the context's
- * stream changes. */
+ * stream changes.  The buffer is one per context: a bloom on another stream
+ * than the last one first waits (on the device) for that one, marked when the
+ * context left its stream. */
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out);
 
 /* The reference's two post passes of a frame, chained as main.cpp:209-214 runs
@@ -300,6 +302,12 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
  * words, pairwise distinct, W*H < 2^30; asynchronous on the context's stream;
  * bloom's scratch as rm_bloom's. */
 rm_status rm_post_chain(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *mid, uint32_t *out);
+
+/* The render kernels' code objects by content (16 hex digits of a SHA-256 of
+ * the translation units that hold them): rocprofv3 counters of a render launch
+ * (profiles/pmc_counters.json) name the build they counted, and bench.py
+ * prices a launch with them only when this hash matches. */
+const char *rm_render_code_hash(void);
 
 /* ---- Weighted row parts: frame row y belongs to a part iff (y mod cycle) - offset
  * lies in [0, run).  Round-robin bands are the special case run = band,

@@ -9,7 +9,7 @@ multi-GPU frame (``frame.py``).
 """
 from ._lib import EXPORTS, LIB_PATH, RmError, lib  # noqa: F401
 from .api import (Comm, Renderer, RenderTexture, Shader, ShaderLoader, comm_get_id, compile_scene,  # noqa: F401
-                  cycle_rows, shard_rows, sharded_layout, wire_capacity, wire_workspace_bytes)
+                  cycle_rows, shard_rows, sharded_layout, wire_capacity, render_code_hash, wire_workspace_bytes)
 from .poses import POSES, S0_POSE  # noqa: F401
 
 # ray-step (sceneSDF) algorithmic FLOP per scene: SURVEY.md 8(d), DESIGN.md

@@ -519,6 +519,12 @@ def _check_out(t, nfloats):
         raise ValueError(f"buffer must be contiguous 32-bit with >= {nfloats} elements")
 
 
+def render_code_hash() -> str:
+    """The render kernels' code objects by content (rm_render_code_hash): the
+    build a PMC counter set was taken with (bench.py)."""
+    return lib().rm_render_code_hash().decode()
+
+
 def wire_capacity(W: int, nrows: int) -> int:
     """Largest wire message of nrows rows of W pixels (rm_wire_capacity)."""
     v = int(lib().rm_wire_capacity(int(W), int(nrows)))

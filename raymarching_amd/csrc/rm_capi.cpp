@@ -80,6 +80,13 @@ struct rm_ctx {
     size_t mips_texels = 0;
     int bloom_runs_w = 0, bloom_runs_h = 0;  // the size whose bloom run tables `mips` holds (0: none)
     hipStream_t bloom_runs_stream = nullptr;
+    // the scratch buffer is shared by the context's streams: when the context
+    // leaves the stream of its last bloom / post chain (bloom_stream), bloom_ev
+    // is recorded there, and a bloom on another stream first waits for it (no
+    // marker per frame; one per leave, and only after a bloom)
+    hipEvent_t bloom_ev = nullptr;
+    hipStream_t bloom_stream = nullptr;
+    bool bloom_pending = false;  // a bloom ran on bloom_stream since bloom_ev was last recorded
     rmplugin::Module plugin;  // the loaded scene plugin (scene == SCENE_PLUGIN)
     uint32_t *tile_order = nullptr;  // rm_set_tile_order (device copy)
     int64_t tile_order_n = 0;
@@ -105,9 +112,22 @@ struct rm_ctx {
         // entry as well; rm_destroy destroys it after the entries are released)
         hipEvent_t left = nullptr;
         uint64_t used = 0;
+        size_t bytes = 0;  // buf's size
     };
     Sched sched[8];
     uint64_t sched_clock = 0;
+    // buffers of evicted adaptive-order entries, each with the marker of its
+    // last use (ev: owned, or a borrowed `done` event); reused by a new entry
+    // once the marker has completed, instead of a host wait at the eviction
+    // (a marker recorded then on a kept stream covers everything queued there
+    // since, e.g. the next pipelined frame)
+    struct Spare {
+        uint32_t *buf = nullptr;
+        size_t bytes = 0;
+        hipEvent_t ev = nullptr;
+        bool own = false;
+    };
+    std::vector<Spare> spare;
 };
 
 namespace {
@@ -502,6 +522,53 @@ hipError_t sched_release(rm_ctx *ctx, rm_ctx::Sched &e) {
     return r;
 }
 
+void spare_free(rm_ctx::Spare &sp) {
+    if (sp.ev) (void)hipEventSynchronize(sp.ev);
+    (void)hipFree(sp.buf);
+    if (sp.own && sp.ev) (void)hipEventDestroy(sp.ev);
+    sp = rm_ctx::Spare();
+}
+
+// Evict an entry without a host wait: its buffer joins ctx->spare with the
+// marker of its last use (sched_release's three cases, recorded or borrowed).
+hipError_t sched_retire(rm_ctx *ctx, rm_ctx::Sched &e, size_t bytes) {
+    if (!e.buf) return sched_release(ctx, e);
+    rm_ctx::Spare sp{e.buf, bytes, nullptr, false};
+    if (e.dirty && (e.stream == ctx->stream || is_kept(ctx, e.stream))) {
+        hipError_t r = hipEventRecord(e.last, e.stream);
+        if (r != hipSuccess) return sched_release(ctx, e);
+        sp.ev = e.last, sp.own = true;
+    } else if (e.left) {
+        sp.ev = e.left;  // (borrowed: destroyed by rm_destroy, after the spares)
+        if (e.last) (void)hipEventDestroy(e.last);
+    } else {
+        sp.ev = e.last, sp.own = true;
+    }
+    if (ctx->spare.size() >= 8) {  // bounded: the oldest is freed (a host wait, rare)
+        spare_free(ctx->spare.front());
+        ctx->spare.erase(ctx->spare.begin());
+    }
+    ctx->spare.push_back(sp);
+    e = rm_ctx::Sched();
+    return hipSuccess;
+}
+
+// A spare buffer of at least `bytes` whose last use has completed, or null.
+uint32_t *spare_take(rm_ctx *ctx, size_t bytes, size_t &got) {
+    for (size_t i = 0; i < ctx->spare.size(); i++) {
+        rm_ctx::Spare &sp = ctx->spare[i];
+        if (sp.bytes < bytes || (sp.ev && hipEventQuery(sp.ev) != hipSuccess)) continue;
+        uint32_t *b = sp.buf;
+        got = sp.bytes;
+        if (sp.own && sp.ev) (void)hipEventDestroy(sp.ev);
+        ctx->spare.erase(ctx->spare.begin() + (long)i);
+        (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+        return b;
+    }
+    (void)hipGetLastError();
+    return nullptr;
+}
+
 // The adaptive-order state of a launch geometry on the ctx stream (least
 // recently used entry recycled), or null when scheduling does not apply.
 rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, int count, rm_status &st) {
@@ -525,9 +592,15 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, const RowPart &part, int ro
         if (e.used < lru->used) lru = &e;
     }
     hipError_t e = hipSuccess;
-    e = sched_release(ctx, *lru);
     // cost[2][n] | order[2][n] | 2 x (hist | cursor) | bucket bytes[n]
-    if (e == hipSuccess) e = hipMalloc(&lru->buf, ((size_t)4 * n + 1024 + ((size_t)n + 3) / 4) * sizeof(uint32_t));
+    const size_t need = ((size_t)4 * n + 1024 + ((size_t)n + 3) / 4) * sizeof(uint32_t);
+    e = sched_retire(ctx, *lru, lru->bytes);
+    size_t got = 0;
+    if (e == hipSuccess && (lru->buf = spare_take(ctx, need, got)) == nullptr) {
+        e = hipMalloc(&lru->buf, need);
+        got = need;
+    }
+    lru->bytes = got;
     if (e == hipSuccess) e = hipMemsetAsync(lru->buf + 4 * (size_t)n, 0, 1024 * sizeof(uint32_t), ctx->stream);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&lru->last, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -789,6 +862,8 @@ rm_status rm_destroy(rm_ctx *ctx) {
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
     }
+    for (rm_ctx::Spare &sp : ctx->spare) spare_free(sp);  // (before the borrowed `done` events go)
+    ctx->spare.clear();
     for (hipEvent_t ev : ctx->retired) {
         (void)hipEventSynchronize(ev);
         (void)hipEventDestroy(ev);
@@ -807,6 +882,7 @@ rm_status rm_destroy(rm_ctx *ctx) {
     }
     if (ctx->staging) (void)hipFree(ctx->staging);
     if (ctx->mips) (void)hipFree(ctx->mips);
+    if (ctx->bloom_ev) (void)hipEventDestroy(ctx->bloom_ev);
     if (ctx->tile_order) (void)hipFree(ctx->tile_order);
     for (rm_ctx::Sched &e : ctx->sched) (void)sched_release(ctx, e);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -911,18 +987,21 @@ rm_status rm_get_params(rm_ctx *ctx, rm_params *p) {
 rm_status rm_set_stream(rm_ctx *ctx, void *stream) {
     if (!ctx) return RM_ERR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // RM_LEAVE_NO_RECORD=1 (analysis only, unsafe: a later release of a
-    // schedule buffer or rm_destroy no longer waits for the old stream's
-    // work): leaving a stream records nothing, which prices the marker
-    // (tools/scale_model.py)
-    static const bool no_record = [] {
-        const char* e = std::getenv("RM_LEAVE_NO_RECORD");
-        return e && e[0] == '1';
-    }();
-    if (no_record) {
-        ctx->stream = s;
-        return RM_OK;
+    if (s != ctx->stream && ctx->bloom_pending && ctx->bloom_stream == ctx->stream) {
+        // the last bloom's scratch use, marked for a bloom on another stream (bloom_scratch)
+        RM_HIP(hipSetDevice(ctx->device));
+        if (!ctx->bloom_ev) RM_HIP(hipEventCreateWithFlags(&ctx->bloom_ev, hipEventDisableTiming));
+        RM_HIP(hipEventRecord(ctx->bloom_ev, ctx->stream));
+        ctx->bloom_pending = false;
     }
+#ifdef RM_ANALYSIS_LEAVE_NO_RECORD
+    // analysis builds only (-DRM_ANALYSIS_LEAVE_NO_RECORD, tools/scale_model.py
+    // prices the marker with it; unsafe: a later release of a schedule buffer or
+    // rm_destroy no longer waits for the old stream's work): leaving a stream
+    // records nothing
+    ctx->stream = s;
+    return RM_OK;
+#endif
     if (s != ctx->stream && ctx->dirty && is_kept(ctx, ctx->stream)) {
         // a kept stream: no marker now (its entries stay dirty, rm_ctx::kept)
         bool listed = false;
@@ -1263,6 +1342,8 @@ rm_status rm_fxaa(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) 
 // run tables can be reused (the last bloom of this context had the same size
 // and stream: same buffer)
 static rm_status bloom_scratch(rm_ctx *ctx, const rm::BloomPlan &plan, int W, int H, bool &cached) {
+    if (ctx->bloom_ev && ctx->bloom_stream != ctx->stream)  // the last bloom ran on another stream
+        RM_HIP(hipStreamWaitEvent(ctx->stream, ctx->bloom_ev, 0));
     if (plan.texels > ctx->mips_texels) {
         if (ctx->mips) RM_HIP(hipFree(ctx->mips));
         ctx->mips = nullptr;
@@ -1275,10 +1356,13 @@ static rm_status bloom_scratch(rm_ctx *ctx, const rm::BloomPlan &plan, int W, in
     ctx->bloom_runs_w = 0;
     return RM_OK;
 }
-static void bloom_done(rm_ctx *ctx, int W, int H) {
+static rm_status bloom_done(rm_ctx *ctx, int W, int H) {
+    ctx->bloom_stream = ctx->stream;
+    ctx->bloom_pending = true;
     ctx->bloom_runs_w = W;
     ctx->bloom_runs_h = H;
     ctx->bloom_runs_stream = ctx->stream;
+    return RM_OK;
 }
 
 rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out) {
@@ -1294,7 +1378,7 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
     if (rm_status st = bloom_scratch(ctx, plan, W, H, cached)) return st;
     hipError_t e = rm::launch_bloom(in, out, ctx->mips, plan, ctx->stream, cached);
     if (e != hipSuccess) return hip_fail(ctx, e, "bloom launch");
-    bloom_done(ctx, W, H);
+    if (rm_status st = bloom_done(ctx, W, H)) return st;
     return mark_done(ctx);
 }
 
@@ -1318,7 +1402,7 @@ rm_status rm_post_chain(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t 
     if (e != hipSuccess) return hip_fail(ctx, e, "post chain: fxaa launch");
     e = rm::launch_bloom(mid, out, ctx->mips, plan, ctx->stream, cached, plan.chain);
     if (e != hipSuccess) return hip_fail(ctx, e, "post chain: bloom launch");
-    bloom_done(ctx, W, H);
+    if (rm_status st = bloom_done(ctx, W, H)) return st;
     return mark_done(ctx);
 }
 

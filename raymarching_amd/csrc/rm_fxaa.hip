@@ -446,18 +446,32 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
     }
 #else
     constexpr int NB = (FXL_TX / BW) * (FXL_TY / BH);  // pixel blocks (rows when BW = 64) per tile
-    for (int b = wv; b < NB; b += 2 * FXL_NW) {
+    constexpr int NPASS = NB / (2 * FXL_NW);                // passes of two blocks per wave
+    static_assert(NB % (2 * FXL_NW) == 0, "whole passes");
+    uint32_t keep[2 * NPASS];  // (l3: the wave's output blocks, for the level-3 epilogue)
+#pragma unroll
+    for (int i = 0; i < NPASS; i++) {
+        const int b = wv + 2 * FXL_NW * i;
         const uint32_t v0 = pixel(b), v1 = pixel(b + FXL_NW);
         const int xa = x0 + px_col(b), ya = y0 + px_row(b), xb = x0 + px_col(b + FXL_NW), yb = y0 + px_row(b + FXL_NW);
         if (xa < W && ya < H) out[(size_t)ya * W + xa] = v0;
         if (xb < W && yb < H) out[(size_t)yb * W + xb] = v1;
-        if constexpr (BW == 8) {
-            if (l3) {  // (chain_fxaa_ok: whole blocks; wave-uniform)
-                const uint32_t m0 = block_mip3(v0), m1 = block_mip3(v1);
-                if (lane == 0) {
-                    const int w3 = W >> 3;
-                    l3[(size_t)(ya >> 3) * w3 + (xa >> 3)] = m0;
-                    l3[(size_t)(yb >> 3) * w3 + (xb >> 3)] = m1;
+        keep[2 * i] = v0;
+        keep[2 * i + 1] = v1;
+    }
+    if constexpr (BW == 8) {
+        // level 3 after the last pass: the blocks' reductions are independent
+        // chains, interleaved (one block's chain alone is latency-bound)
+        if (l3) {  // (chain_fxaa_ok: whole blocks; wave-uniform)
+            uint32_t m[2 * NPASS];
+#pragma unroll
+            for (int k = 0; k < 2 * NPASS; k++) m[k] = block_mip3(keep[k]);
+            if (lane == 0) {
+                const int w3 = W >> 3;
+#pragma unroll
+                for (int k = 0; k < 2 * NPASS; k++) {
+                    const int b = wv + FXL_NW * k;  // pass k / 2, block (k & 1): wv + 2 NW (k / 2) + NW (k & 1)
+                    l3[(size_t)((y0 >> 3) + b / NBX) * w3 + (x0 >> 3) + b % NBX] = m[k];
                 }
             }
         }

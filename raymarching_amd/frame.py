@@ -659,8 +659,8 @@ class DeltaFrame(DistributedFrame):
                 allsz = torch.empty(self.world, dtype=torch.int64, device=self.dev)
                 dist.all_gather_into_tensor(allsz, sz, group=self.group)
                 sizes = [int(v) for v in allsz.cpu()]
+                self._check_sizes(sizes)  # (every rank: all fail together, before any send or receive)
                 if self.rank == 0:
-                    self._check_sizes(slot, sizes)
                     if self.decoded_recorded[slot]:
                         self.ctrl.wait_event(self.decoded[slot])  # the slot's last decode has read its buffers
                     ops = [dist.P2POp(dist.irecv, self.recv[slot][q][: sizes[q]], q, group=self.group)
@@ -671,8 +671,8 @@ class DeltaFrame(DistributedFrame):
         allsz = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
         dist.all_gather(allsz, torch.tensor([mine], dtype=torch.int64), group=self.group)
         sizes = [int(v[0]) for v in allsz]
+        self._check_sizes(sizes)  # (every rank: all fail together, before any send or receive)
         if self.rank == 0:
-            self._check_sizes(slot, sizes)
             for q in range(1, self.world):
                 buf = torch.empty(sizes[q], dtype=torch.uint8)
                 dist.recv(buf, src=q, group=self.group)
@@ -681,13 +681,16 @@ class DeltaFrame(DistributedFrame):
             dist.send(self.msg[slot][:mine].cpu(), dst=0, group=self.group)
         return sizes, []
 
-    def _check_sizes(self, slot, sizes):
-        """The peers' message sizes against the receive buffers (wire
-        capacity): a larger one would be truncated and the send/receive
-        lengths would no longer match (a hang or a corrupt decode), so it
-        fails here instead."""
+    def _check_sizes(self, sizes):
+        """The ranks' message sizes against the wire capacity of their parts
+        (rank 0's receive buffers): a larger one would be truncated and the
+        send/receive lengths would no longer match (a hang or a corrupt
+        decode), so it fails here instead -- on every rank, which all hold
+        the gathered sizes, so no peer is left blocked in a send until the
+        process group's timeout."""
+        from .api import wire_capacity
         for q in range(1, self.world):
-            cap = self.recv[slot][q].numel()
+            cap = wire_capacity(self.plan.W, self.plan.count(q))
             if not 0 <= sizes[q] <= cap:
                 raise RuntimeError(f"DeltaFrame: rank {q} reports a {sizes[q]}-byte message; the receive buffer "
                                    f"holds {cap} (wire capacity)")

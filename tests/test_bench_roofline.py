@@ -168,3 +168,17 @@ def test_post_bytes_model():
     assert ch["total"] < bench.post_bytes(4096, 4096, "fxaa")["total"] + bl["total"] - 0.9 * px
     # lod <= 0: one kernel, frame in and out
     assert bench.post_bytes(64, 16, "bloom")["kernels"] == {"bloom": 2 * 4 * 64 * 16}
+
+
+def test_pmc_of_another_build_nulls_frac_on_every_path():
+    """Counters tagged with another build's render code hash price no launch:
+    not the counted frame, not a rank's share, not a walk."""
+    pmc = dict(C3, render_code_hash="0123456789abcdef")
+    ms = C3["avg_kernel_ns_trace"] / 1e6
+    for exact in (True, False):
+        r = bench.roofline(pmc, ms, C3["executed_ray_steps_per_launch"] // 2, 0, None, None, exact=exact,
+                           rows_frac=0.5, code_hash="fedcba9876543210")
+        assert r["frac"] is None and "render code" in r["frac_null_reason"]
+    # the same hash (or none recorded) prices as before
+    r = bench.roofline(pmc, ms, C3["executed_ray_steps_per_launch"], 0, None, None, code_hash="0123456789abcdef")
+    assert r["frac"] is not None

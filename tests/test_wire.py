@@ -121,3 +121,20 @@ def test_gpu_wire_rejects_bad_parts(R, torch_cuda):
         R.wire_decode(64, 8, 4, 3, 2, 1, msg, frame)  # offset + run > cycle
     with pytest.raises(rm.RmError):
         R.wire_decode(64, 8, 4, 0, 2, 5, msg, frame)  # more rows than the part has
+
+
+def test_delta_frame_size_check_on_every_rank():
+    """DeltaFrame._check_sizes needs only the plan (no receive buffers), so
+    every rank runs it on the gathered sizes before any send or receive: a
+    rank reporting more than its part's wire capacity fails them all."""
+    from types import SimpleNamespace
+
+    from raymarching_amd.frame import DeltaFrame, ShardPlan
+    plan = ShardPlan(4096, 4096, 16, 3)
+    stub = SimpleNamespace(world=3, plan=plan)
+    caps = [rm.wire_capacity(4096, plan.count(q)) for q in range(3)]
+    DeltaFrame._check_sizes(stub, [0, caps[1], 17])
+    with pytest.raises(RuntimeError, match="rank 2"):
+        DeltaFrame._check_sizes(stub, [0, 5, caps[2] + 1])
+    with pytest.raises(RuntimeError, match="rank 1"):
+        DeltaFrame._check_sizes(stub, [0, -1, 5])

@@ -14,6 +14,9 @@ Per launch of the render kernel:
   flop_lanes = flop_exec * active_lane_frac: FP32 FLOP done by active lanes
   clock_hz = GRBM_GUI_ACTIVE / 8 XCDs / the kernel's average duration (from
       the kernel-trace stats of the same command)
+  render_code_hash = rm_render_code_hash() of the library in the tree (the
+      build whose launch was counted: run this where the profile ran, with
+      the same librm.so)
   executed_ray_steps_per_launch = config.executed_ray_steps_per_frame of the
       bench line the same command printed (BENCH_LOG: a file whose last JSON
       line is bench.py's), so bench.py can price a rank's share of the frame
@@ -34,6 +37,12 @@ v = d[k]
 avg_ns = [float(r["AverageNs"]) for r in csv.DictReader(open(stats)) if ksub in r["Name"]][0]
 entry = {"kernel": k, "source": os.path.relpath(summ), "kernel_stats": os.path.relpath(stats),
          "avg_kernel_ns_trace": avg_ns}
+try:  # the build these counters were taken with (bench.py prices a launch with them only on a match)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    import raymarching_amd as rm
+    entry["render_code_hash"] = rm.render_code_hash()
+except Exception as e:  # noqa: BLE001 (the library is not built here: no hash, bench falls back to the duration check)
+    print("no render code hash:", e, file=sys.stderr)
 if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
     entry.update(FETCH_SIZE_KiB=v["FETCH_SIZE"], WRITE_SIZE_KiB=v["WRITE_SIZE"],
                  hbm_bytes_per_launch=(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024)

@@ -1,5 +1,5 @@
 # PMC passes (one rocprofv3 run per counter group) over tools/post_probe.py.
-# Usage: bash tools/pmc_post.sh fxaa|bloom ; summaries via tools/pmc_parse.py
+# Usage: bash tools/pmc_post.sh fxaa|bloom|post_chain ; summaries via tools/pmc_parse.py
 set -u
 export TMPDIR=/tmp
 P=${1:-fxaa}
