@@ -211,10 +211,7 @@ def post_plan(W, H):
     """bloom's level pair and passes as rm_post.hip's bloom_plan computes them
     (lod = log2(0.05 H) in float32, levels d1 = floor(lod), d2 = d1 + 1), and
     which mip path a W x H frame takes: the exact-halving pyramid from level
-    s0 (W, H multiples of 2^d2, 5..8 levels), per-level resamples otherwise;
-    chain: rm_post_chain's fused path (the FXAA kernel writes level 3 and the
-    pyramid starts there: d2 - 3 in [5, 8], W, H multiples of 2^d2 and of the
-    FXAA tile 64 x 32, W, H <= 2^20)."""
+    s0 (W, H multiples of 2^d2, 5..8 levels), per-level resamples otherwise."""
     import numpy as np
 
     q = max(W, H).bit_length() - 1
@@ -231,10 +228,8 @@ def post_plan(W, H):
     div = W % T2 == 0 and H % T2 == 0
     s0 = max(d2 - 8, 0)
     pyramid = lod > 0 and d2 - s0 >= 5 and div
-    chain = (lod > 0 and 5 <= d2 - 3 <= 8 and div and W % 64 == 0 and H % 32 == 0 and W <= 1 << 20
-             and H <= 1 << 20)
     nruns = [min(n, 5 * lw + 1) for n, lw in ((W, w[d1]), (H, h[d1]), (W, w[d2]), (H, h[d2]))] if lod > 0 else []
-    return dict(lod=lod, d1=d1, d2=d2, w=w, h=h, s0=s0, pyramid=pyramid, chain=chain, nruns=nruns)
+    return dict(lod=lod, d1=d1, d2=d2, w=w, h=h, s0=s0, pyramid=pyramid, nruns=nruns)
 
 
 def post_bytes(W, H, which):
@@ -256,7 +251,7 @@ def post_bytes(W, H, which):
     px = 4 * W * H
     k = {}
     if which in ("fxaa", "chain"):
-        k["fxaa"] = 2 * px + (px // 64 if which == "chain" and P["chain"] else 0)
+        k["fxaa"] = 2 * px
     if which == "fxaa":
         return dict(kernels=k, total=sum(k.values()), plan=P)
     if P["lod"] <= 0:
@@ -264,9 +259,7 @@ def post_bytes(W, H, which):
         return dict(kernels=k, total=sum(k.values()), plan=P)
     w, h, d1, d2 = P["w"], P["h"], P["d1"], P["d2"]
     lv = lambda j: 4 * w[j] * h[j]  # noqa: E731
-    if which == "chain" and P["chain"]:
-        k["mips"] = lv(3) + lv(d1) + lv(d2)
-    elif P["pyramid"]:
+    if P["pyramid"]:
         s0 = P["s0"]
         k["mips"] = sum(lv(j - 1) + lv(j) for j in range(1, s0 + 1)) + lv(s0) + lv(d1) + lv(d2)
     else:
@@ -377,7 +370,6 @@ def time_pipeline(r, W, H, stream, counters, render_ms, reps=20):
     nd = int((ref != out).sum())
     chain = _post_line("post chain: fxaa + mips + bloom (main.cpp:209-214, rm_post_chain)", chain_ms, W, H, "chain",
                        counters)
-    chain["fused_level3"] = post_plan(W, H)["chain"]
     return {"pipeline_ms": pipe_ms, "pipeline_frames_per_s": 1e3 / pipe_ms,
             "render_ms": render_ms, "post_chain": chain,
             "chain_check": {"result": "bit-exact" if nd == 0 else "MISMATCH", "pixels_differing": nd,

@@ -293,14 +293,10 @@ rm_status rm_bloom(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *out)
 
 /* The reference's two post passes of a frame, chained as main.cpp:209-214 runs
  * them: FXAA of `in` into `mid` (post_shader into postTexture), then bloom of
- * `mid` into `out` (postTexture.generateMipmap, post_bloom.apply).  The same
- * bits as rm_fxaa(in -> mid) followed by rm_bloom(mid -> out); where the frame
- * allows (W, H multiples of 2^d2 with bloom's levels d2 - 3 in [5, 8], e.g.
- * 4096 x 4096, and of the FXAA kernel's 64 x 32 tile) the FXAA kernel also
- * writes mip level 3 of `mid` from registers and the mip pyramid starts there
- * instead of re-reading `mid`.  Device buffers of W x H RGBA8
- * words, pairwise distinct, W*H < 2^30; asynchronous on the context's stream;
- * bloom's scratch as rm_bloom's. */
+ * `mid` into `out` (postTexture.generateMipmap, post_bloom.apply): the same
+ * bits as rm_fxaa(in -> mid) followed by rm_bloom(mid -> out), in one call.
+ * Device buffers of W x H RGBA8 words, pairwise distinct, W*H < 2^30;
+ * asynchronous on the context's stream; bloom's scratch as rm_bloom's. */
 rm_status rm_post_chain(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t *mid, uint32_t *out);
 
 /* The render kernels' code objects by content (16 hex digits of a SHA-256 of
@@ -331,17 +327,18 @@ rm_status rm_deinterleave_cycle_rgb8(rm_ctx *ctx, int W, int H, int cycle, int n
                                      uint32_t *out);
 
 /* ---- Compressed wire of RGBA8 row parts ----
- * A lossless delta code per 64-pixel row segment (first pixel, left
- * differences as per-channel bit planes); alpha is not sent (the root stores
- * 255).  rm_wire_encode: nrows packed RGBA8 rows -> msg (at most
- * rm_wire_capacity bytes), using a caller-owned device workspace of
- * rm_wire_workspace_bytes; the message size (also its first 8 bytes) is
- * written to the device int64 *size_out when non-null (asynchronous, ctx
- * stream).  rm_wire_decode: a message of nrows rows of the cyclic part
- * (cycle, offset, run) into those rows of the W x H RGBA8 frame.
+ * A lossless code per 8x8-pixel tile of a part's packed rows: the first
+ * pixel, then per channel the differences to the left neighbour (to the one
+ * above in the tile's first column) as bit planes of their zig-zagged bytes;
+ * alpha is not sent (the root stores 255).  rm_wire_encode: nrows packed
+ * RGBA8 rows -> msg (at most rm_wire_capacity bytes), using a caller-owned
+ * device workspace of rm_wire_workspace_bytes; the message size (also its
+ * first 8 bytes) is written to the device int64 *size_out when non-null
+ * (asynchronous, ctx stream).  rm_wire_decode: a message of nrows rows of the
+ * cyclic part (cycle, offset, run) into those rows of the W x H RGBA8 frame.
  * rm_scatter_part_rgba8: a part's packed RGBA8 rows into their frame rows
  * (the root's own part).  Capacity/workspace return -1 for bad sizes
- * (W <= 2^18; a message holds at most 65535 rows). */
+ * (W <= 2^18). */
 int64_t rm_wire_capacity(int W, int nrows);
 int64_t rm_wire_workspace_bytes(int W, int nrows);
 rm_status rm_wire_encode(rm_ctx *ctx, int W, int nrows, const uint32_t *rows, uint8_t *msg, void *workspace,
@@ -355,6 +352,17 @@ rm_status rm_scatter_part_rgba8(rm_ctx *ctx, int W, int H, int cycle, int offset
  * device pointers. */
 rm_status rm_wire_decode_parts(rm_ctx *ctx, int W, int H, int cycle, int nparts, const int *offsets, const int *runs,
                                const int *nrows, const uint8_t *const *msgs, uint32_t *frame);
+
+/* rm_render_cycle_rows_rgba8 and rm_wire_encode in one: the render kernel
+ * encodes each of its 8x8-pixel tiles for the wire from registers (its own
+ * epilogue: the rows are never written), then the tiles' words are scanned
+ * and compacted into msg; msg, workspace and *size_out as rm_wire_encode's for
+ * row_count rows, and the message is byte for byte rm_wire_encode's of the
+ * rows rm_render_cycle_rows_rgba8 renders.  Built-in scenes (a plugin part:
+ * the two calls).  The non-root ranks of a sharded frame call this instead of
+ * rendering rows they only send. */
+rm_status rm_render_cycle_rows_wire(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int row_begin,
+                                    int row_count, uint8_t *msg, void *workspace, int64_t *size_out, rm_stats *stats);
 
 /* ---- Multi-GPU: row-sharded frames over RCCL ----
  * The reference renders one frame on one GPU (main.cpp:196-207); here a frame's

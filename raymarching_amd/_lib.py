@@ -23,7 +23,7 @@ EXPORTS = ("rm_create", "rm_destroy", "rm_load_scene", "rm_set_uniform1f", "rm_s
            "rm_synchronize",
            "rm_render", "rm_render_band", "rm_render_rows", "rm_shard_rows", "rm_deinterleave", "rm_deinterleave_rgba8",
            "rm_pack_rgba8", "rm_pack_rgb8", "rm_deinterleave_rgb8",
-           "rm_render_rgba8", "rm_render_accumulate", "rm_render_accumulate_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_post_chain", "rm_render_code_hash", "rm_last_error", "rm_status_string",
+           "rm_render_rgba8", "rm_render_accumulate", "rm_render_accumulate_rgba8", "rm_render_band_rgba8", "rm_render_rows_rgba8", "rm_fxaa", "rm_bloom", "rm_post_chain", "rm_render_code_hash", "rm_render_cycle_rows_wire", "rm_last_error", "rm_status_string",
            "rm_compile_scene", "rm_scene_eval", "rm_render_step_map", "rm_sharded_layout", "rm_comm_get_id",
            "rm_comm_init_rank", "rm_comm_init_all", "rm_comm_destroy", "rm_render_sharded", "rm_render_sharded_all",
            "rm_set_tile_order", "rm_tile_grid", "rm_comm_info", "rm_abi_version", "rm_cycle_rows",
@@ -123,6 +123,8 @@ def lib() -> ctypes.CDLL:
         "rm_bloom": ([vp, c.c_int, c.c_int, vp, vp], c.c_int),
         "rm_post_chain": ([vp, c.c_int, c.c_int, vp, vp, vp], c.c_int),
         "rm_render_code_hash": ([], cp),
+        "rm_render_cycle_rows_wire": ([vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp, vp,
+                                       c.POINTER(RmStats)], c.c_int),
         "rm_compile_scene": ([cp, vp, c.c_size_t], c.c_int),
         "rm_scene_eval": ([vp, vp, c.c_int64, vp, vp], c.c_int),
         "rm_sharded_layout": ([c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(RmShardLayout)], c.c_int),

@@ -227,6 +227,27 @@ class Renderer:
                                                self._ptr(out)), self._ctx)
         return out
 
+    def render_cycle_rows_wire(self, W, H, cycle, offset, run, row_begin, row_count, msg, workspace, size_out=None,
+                               stats=False):
+        """render_cycle_rows's RGBA8 rows as the compressed wire's message,
+        encoded by the render kernel's epilogue (rm_render_cycle_rows_wire):
+        `msg` uint8 of wire_capacity(W, row_count) bytes, `workspace` of
+        wire_workspace_bytes(W, row_count), `size_out` an optional int64
+        device tensor [1] for the message size (asynchronously)."""
+        torch = _torch()
+        if msg.dtype != torch.uint8 or msg.numel() < wire_capacity(W, row_count) or not msg.is_contiguous():
+            raise ValueError("render_cycle_rows_wire: msg must be a contiguous uint8 tensor of wire_capacity bytes")
+        if workspace.numel() * workspace.element_size() < wire_workspace_bytes(W, row_count):
+            raise ValueError("render_cycle_rows_wire: workspace too small")
+        if size_out is not None and (size_out.dtype != torch.int64 or size_out.numel() < 1):
+            raise ValueError("render_cycle_rows_wire: size_out must be an int64 tensor")
+        s = RmStats()
+        check(lib().rm_render_cycle_rows_wire(self._ctx, int(W), int(H), int(cycle), int(offset), int(run),
+                                              int(row_begin), int(row_count), self._ptr(msg), self._ptr(workspace),
+                                              self._ptr(size_out) if size_out is not None else None,
+                                              ctypes.byref(s) if stats else None), self._ctx)
+        return (msg, s.as_dict()) if stats else msg
+
     def wire_encode(self, rows, msg, workspace, size_out=None):
         """Compressed wire of packed RGBA8 rows (int32 [n, W]) into the uint8
         `msg` (>= wire_capacity bytes), with a uint8 `workspace` of

@@ -616,9 +616,18 @@ rm_ctx::Sched *sched_slot(rm_ctx *ctx, int W, int H, const RowPart &part, int ro
     return lru;
 }
 
+// rm_render_cycle_rows_wire: the compressed wire's message instead of pixels
+// (`out` is then the tile-slot workspace, rm_wire_tile.h)
+struct WireOut {
+    uint8_t *msg;
+    long long *size_out;
+};
+
 rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, int count, void *out, bool rgba8,
-                     rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false) {
+                     rm_stats *stats, uint32_t *evmap = nullptr, bool accum = false, const WireOut *wire = nullptr) {
     rm::TraceRange range("rm_render");
+    // the wire's tile code runs in one-wave 8x8 tiles (rm_render_direct.h)
+    const int kernel = wire ? (int)rm::KERNEL_TILE8 : pick_kernel(ctx);
     FrameConst F = frame_const(ctx, W, H, part, count);
     F.row0 = row0;
     F.evals_map = evmap;
@@ -630,8 +639,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
     }
     rm_ctx::Sched *sc = nullptr;
     if (ctx->tile_order) {  // an explicit order wins
-        const rm::TileGrid g =
-            rm::tile_grid(ctx->scene == rm::SCENE_PLUGIN ? (int)rm::KERNEL_TILE8 : pick_kernel(ctx), W, count);
+        const rm::TileGrid g = rm::tile_grid(ctx->scene == rm::SCENE_PLUGIN ? (int)rm::KERNEL_TILE8 : kernel, W, count);
         if ((int64_t)g.x * g.y == ctx->tile_order_n) F.tile_order = ctx->tile_order;
     } else {
         rm_status st;
@@ -652,7 +660,7 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
         }
     }
     rm_ctx::PersistBlock *pb = nullptr;
-    if (ctx->scene != rm::SCENE_PLUGIN && pick_kernel(ctx) == rm::KERNEL_PERSIST) {
+    if (ctx->scene != rm::SCENE_PLUGIN && kernel == rm::KERNEL_PERSIST) {
         // this stream's counters, zeroed once; each launch leaves them zeroed
         rm_status st = persist_block(ctx, pb);
         if (st != RM_OK) return st;
@@ -662,11 +670,17 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
     if (cnt) RM_HIP(hipMemsetAsync(ctx->d_evals, 0, 3 * sizeof(unsigned long long), ctx->stream));
     if (stats) RM_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     hipError_t e =
-        ctx->scene == rm::SCENE_PLUGIN
+        wire ? rm::launch_render_wire(ctx->scene, F, static_cast<rm::WireTile *>(out), cnt ? ctx->d_evals : nullptr,
+                                      ctx->stream)
+        : ctx->scene == rm::SCENE_PLUGIN
             ? rmplugin::launch_render(ctx->plugin, F, out, rgba8, cnt ? ctx->d_evals : nullptr, ctx->stream)
-            : rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, pick_kernel(ctx), ctx->stream);
+            : rm::launch_render(ctx->scene, F, out, rgba8, cnt ? ctx->d_evals : nullptr, kernel, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "render kernel launch");
     if (stats) RM_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    if (wire) {  // the offset table, the message size, the payload (rm_wire.hip)
+        e = rm::launch_wire_finish(out, W, count, wire->msg, wire->size_out, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "wire scan/compact launch");
+    }
     if (pb) RM_HIP(hipEventRecord(pb->last, ctx->stream));
     if (sc && F.tile_cost) {  // sort this launch's durations, on its stream right after it
         const size_t slot = (sc->k / (uint64_t)sched_period()) & 1;
@@ -700,8 +714,8 @@ rm_status render_dev(rm_ctx *ctx, int W, int H, const RowPart &part, int row0, i
                                                             : RM_DISPATCH_ADAPTIVE;
         // the latency tiles: scene T, an ordered launch of one-wave tiles
         // (rm_render_direct.h render_tile_at)
-        if (F.tile_order && ctx->scene == rm::SCENE_T && pick_kernel(ctx) != rm::KERNEL_TILE16) {
-            const rm::TileGrid g = rm::tile_grid(pick_kernel(ctx), W, count);
+        if (F.tile_order && ctx->scene == rm::SCENE_T && kernel != rm::KERNEL_TILE16) {
+            const rm::TileGrid g = rm::tile_grid(kernel, W, count);
             stats->lat_tiles = std::min(F.lat_tiles, g.x * g.y);
         }
     }
@@ -1120,6 +1134,36 @@ rm_status rm_render_cycle_rows_rgba8(rm_ctx *ctx, int W, int H, int cycle, int o
     return render_part(ctx, W, H, p, row_begin, row_count, out, true, stats);
 }
 
+rm_status rm_render_cycle_rows_wire(rm_ctx *ctx, int W, int H, int cycle, int offset, int run, int row_begin,
+                                    int row_count, uint8_t *msg, void *workspace, int64_t *size_out, rm_stats *stats) {
+    RowPart p;
+    if (!ctx) return RM_ERR_INVALID_ARGUMENT;
+    if (!cycle_part(cycle, offset, run, p) || row_count < 0 || !msg || !workspace || W <= 0 || W > (1 << 18))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_cycle_rows_wire: bad arguments");
+    if (ctx->scene < 0) return fail(ctx, RM_ERR_NO_SCENE, "no scene loaded (rm_load_scene)");
+    if (ctx->scene == rm::SCENE_PLUGIN)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT,
+                    "rm_render_cycle_rows_wire: built-in scenes only (a plugin part: rm_render_cycle_rows_rgba8 + "
+                    "rm_wire_encode)");
+    if (!is_device_ptr(msg) || !is_device_ptr(workspace) || (size_out && !is_device_ptr(size_out)))
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_cycle_rows_wire: device pointers required");
+    const int n = rows_of_part(H, p);
+    if (row_begin < 0 || row_begin + row_count > n)
+        return fail(ctx, RM_ERR_INVALID_ARGUMENT, "rm_render_cycle_rows_wire: packed row range outside the part");
+    RM_HIP(hipSetDevice(ctx->device));
+    const WireOut wo{msg, reinterpret_cast<long long *>(size_out)};
+    if (row_count == 0) {  // an empty message (the table of no tiles)
+        hipError_t e = rm::launch_wire_finish(workspace, W, 0, msg, wo.size_out, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "wire scan launch");
+        if (stats) {
+            std::memset(stats, 0, sizeof(*stats));
+            stats->scene = ctx->scene;
+        }
+        return mark_done(ctx);
+    }
+    return render_dev(ctx, W, H, p, row_begin, row_count, workspace, true, stats, nullptr, false, &wo);
+}
+
 rm_status rm_deinterleave_cycle_rgb8(rm_ctx *ctx, int W, int H, int cycle, int nparts, const int *offsets,
                                      const int *runs, const int64_t *part_bytes, const uint8_t *gathered,
                                      uint32_t *out) {
@@ -1395,12 +1439,11 @@ rm_status rm_post_chain(rm_ctx *ctx, int W, int H, const uint32_t *in, uint32_t 
     const rm::BloomPlan plan = rm::bloom_plan(W, H);
     bool cached = false;
     if (rm_status st = bloom_scratch(ctx, plan, W, H, cached)) return st;
-    // main.cpp:209-214: FXAA into postTexture, its mip chain, bloom of it; with
-    // plan.chain the FXAA kernel also writes mip level 3 and the pyramid starts
-    // there (no re-read of the FXAA frame for the mips)
-    hipError_t e = rm::launch_fxaa(in, mid, W, H, ctx->stream, plan.chain ? ctx->mips + plan.offset[3] : nullptr);
+    // main.cpp:209-214: FXAA into postTexture, its mip chain, bloom of it
+    // (the mips from FXAA's registers measured slower)
+    hipError_t e = rm::launch_fxaa(in, mid, W, H, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "post chain: fxaa launch");
-    e = rm::launch_bloom(mid, out, ctx->mips, plan, ctx->stream, cached, plan.chain);
+    e = rm::launch_bloom(mid, out, ctx->mips, plan, ctx->stream, cached);
     if (e != hipSuccess) return hip_fail(ctx, e, "post chain: bloom launch");
     if (rm_status st = bloom_done(ctx, W, H)) return st;
     return mark_done(ctx);

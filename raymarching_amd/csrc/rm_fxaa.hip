@@ -168,52 +168,8 @@ __device__ __forceinline__ int floor_i32(float v) {  // (int)floorf(v) for |v| <
     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
     return r;
 }
-// l3 (rm_post_chain, BloomPlan::chain): every 8x8-pixel block of the output
-// also as one texel of its mip level 3, formed from the block's registers.
-// The lanes of a block hold pixel (lane & 7, lane >> 3), so level k's 2x2
-// groups are lanes l, l ^ a, l ^ b, l ^ a ^ b with (a, b) = (1, 8), (2, 16),
-// (4, 32).  mip_mean4's per-channel sums (two 16-bit fields per word) are
-// formed by two pair sums x + x(l ^ a), then + x(l ^ b), with cross-lane VALU
-// only (no LDS): DPP quad_perm for a = 1, 2, row_ror:8 for b = 8 (rows of 16
-// lanes: i + 8 mod 16 = i ^ 8), row_ror:4 for a = 4 (i + 4 mod 16 = i ^ 4 on
-// the lanes whose result is used, i & 7 < 4), and v_permlane16/32_swap for b
-// = 16, 32 (the two swapped halves of a word pair sum to x + x(l ^ b) on every
-// lane).  Lane 0 ends with the texel bloom's mip pyramid computes from the
-// stored frame: the same sums and roundings, the same bits.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_pair_sum(uint32_t x) {
-    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
-}
-__device__ __forceinline__ uint32_t swap16_pair_sum(uint32_t x) {
-    const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return p[0] + p[1];
-}
-__device__ __forceinline__ uint32_t swap32_pair_sum(uint32_t x) {
-    const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return p[0] + p[1];
-}
-__device__ __forceinline__ uint32_t mean4_round(uint32_t lo, uint32_t hi) {  // mip_mean4's rounding of the sums
-    const uint32_t m = 0x00FF00FFu, one = 0x00010001u;
-    return (((lo + one + ((lo >> 2) & one)) >> 2) & m) | ((((hi + one + ((hi >> 2) & one)) >> 2) & m) << 8);
-}
-__device__ __forceinline__ uint32_t block_mip3(uint32_t v) {
-    constexpr uint32_t m = 0x00FF00FFu;
-    constexpr int QP_X1 = 0xB1, QP_X2 = 0x4E, ROR8 = 0x128, ROR4 = 0x124;  // quad_perm [1,0,3,2], [2,3,0,1]
-    uint32_t lo = v & m, hi = (v >> 8) & m;
-    lo = dpp_pair_sum<ROR8>(dpp_pair_sum<QP_X1>(lo));
-    hi = dpp_pair_sum<ROR8>(dpp_pair_sum<QP_X1>(hi));
-    v = mean4_round(lo, hi);  // level 1 (lanes with bits 0, 3 clear)
-    lo = v & m, hi = (v >> 8) & m;
-    lo = swap16_pair_sum(dpp_pair_sum<QP_X2>(lo));
-    hi = swap16_pair_sum(dpp_pair_sum<QP_X2>(hi));
-    v = mean4_round(lo, hi);  // level 2 (bits 0, 1, 3, 4 clear)
-    lo = v & m, hi = (v >> 8) & m;
-    lo = swap32_pair_sum(dpp_pair_sum<ROR4>(lo));
-    hi = swap32_pair_sum(dpp_pair_sum<ROR4>(hi));
-    return mean4_round(lo, hi);  // level 3 (lane 0)
-}
 __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                          int W, int H, uint32_t* __restrict__ l3) {
+                                                          int W, int H) {
 #if RM_FXAA_F4
     // RM_FXAA_F4: each staged texel as the floats GL reads (r, g, b) and its
     // luma, plus its alpha byte: a span tap is one 16-byte LDS read instead of
@@ -446,35 +402,11 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
     }
 #else
     constexpr int NB = (FXL_TX / BW) * (FXL_TY / BH);  // pixel blocks (rows when BW = 64) per tile
-    constexpr int NPASS = NB / (2 * FXL_NW);                // passes of two blocks per wave
-    static_assert(NB % (2 * FXL_NW) == 0, "whole passes");
-    uint32_t keep[2 * NPASS];  // (l3: the wave's output blocks, for the level-3 epilogue)
-#pragma unroll
-    for (int i = 0; i < NPASS; i++) {
-        const int b = wv + 2 * FXL_NW * i;
+    for (int b = wv; b < NB; b += 2 * FXL_NW) {
         const uint32_t v0 = pixel(b), v1 = pixel(b + FXL_NW);
         const int xa = x0 + px_col(b), ya = y0 + px_row(b), xb = x0 + px_col(b + FXL_NW), yb = y0 + px_row(b + FXL_NW);
         if (xa < W && ya < H) out[(size_t)ya * W + xa] = v0;
         if (xb < W && yb < H) out[(size_t)yb * W + xb] = v1;
-        keep[2 * i] = v0;
-        keep[2 * i + 1] = v1;
-    }
-    if constexpr (BW == 8) {
-        // level 3 after the last pass: the blocks' reductions are independent
-        // chains, interleaved (one block's chain alone is latency-bound)
-        if (l3) {  // (chain_fxaa_ok: whole blocks; wave-uniform)
-            uint32_t m[2 * NPASS];
-#pragma unroll
-            for (int k = 0; k < 2 * NPASS; k++) m[k] = block_mip3(keep[k]);
-            if (lane == 0) {
-                const int w3 = W >> 3;
-#pragma unroll
-                for (int k = 0; k < 2 * NPASS; k++) {
-                    const int b = wv + FXL_NW * k;  // pass k / 2, block (k & 1): wv + 2 NW (k / 2) + NW (k & 1)
-                    l3[(size_t)((y0 >> 3) + b / NBX) * w3 + (x0 >> 3) + b % NBX] = m[k];
-                }
-            }
-        }
     }
 #endif
 }
@@ -482,18 +414,11 @@ __global__ __launch_bounds__(FXL_NT) void rm_fxaa_lds_kernel(const uint32_t* __r
 #ifndef RM_FXAA_LDS
 #define RM_FXAA_LDS 1
 #endif
-// the LDS kernel's 8x8 blocks tile the frame exactly (its level-3 epilogue)
-bool chain_fxaa_ok(int W, int H) {
-    return RM_FXAA_LDS && RM_FXAA_BW == 8 && RM_FXAA_ROWS == 2 && W <= FXL_MAX_DIM && H <= FXL_MAX_DIM &&
-           W % FXL_TX == 0 && H % FXL_TY == 0;
-}
-
-hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s, uint32_t* l3) {
+hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s) {
     if (W <= 0 || H <= 0) return hipSuccess;
-    if (l3 && !chain_fxaa_ok(W, H)) return hipErrorInvalidValue;
     if (RM_FXAA_LDS && W <= FXL_MAX_DIM && H <= FXL_MAX_DIM) {
         dim3 grid((W + FXL_TX - 1) / FXL_TX, (H + FXL_TY - 1) / FXL_TY);
-        hipLaunchKernelGGL(rm_fxaa_lds_kernel, grid, dim3(FXL_NT), 0, s, in, out, W, H, l3);
+        hipLaunchKernelGGL(rm_fxaa_lds_kernel, grid, dim3(FXL_NT), 0, s, in, out, W, H);
         return hipGetLastError();
     }
     dim3 grid((W + FXAA_TX - 1) / FXAA_TX, (H + FXAA_TY - 1) / FXAA_TY);

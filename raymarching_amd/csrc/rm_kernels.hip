@@ -252,6 +252,25 @@ hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, 
     }
 }
 
+#define RM_WIRE_LAUNCHER(name) \
+    hipError_t name(const FrameConst& F, WireTile* slots, unsigned long long* evals, hipStream_t s);
+RM_WIRE_LAUNCHER(launch_wire_s0)
+RM_WIRE_LAUNCHER(launch_wire_t)
+RM_WIRE_LAUNCHER(launch_wire_o)
+RM_WIRE_LAUNCHER(launch_wire_og)
+
+hipError_t launch_render_wire(int scene, const FrameConst& F, WireTile* slots, unsigned long long* evals,
+                              hipStream_t s) {
+    if (F.W <= 0 || F.nrows <= 0) return hipSuccess;
+    switch (scene) {
+    case SCENE_S0: return launch_wire_s0(F, slots, evals, s);
+    case SCENE_T: return launch_wire_t(F, slots, evals, s);
+    case SCENE_O: return launch_wire_o(F, slots, evals, s);
+    case SCENE_OG: return launch_wire_og(F, slots, evals, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 #define RM_EVAL_LAUNCHER(name) \
     hipError_t name(const FrameConst& F, const float* pts, long long n, float* dist, float* mat, hipStream_t s);
 RM_EVAL_LAUNCHER(launch_eval_s0)

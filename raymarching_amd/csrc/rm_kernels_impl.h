@@ -92,6 +92,13 @@ hipError_t launch_tiling(const FrameConst& F, OUT* out, unsigned long long* eval
     return launch_direct<SC, KERNEL_TILE8>(F, out, evals, s);
 }
 
+// the compressed wire's tile slots (rm_wire_tile.h) instead of pixels: the
+// one-wave 8x8 tiling only
+template <int SC>
+hipError_t launch_scene_wire(const FrameConst& F, WireTile* slots, unsigned long long* evals, hipStream_t s) {
+    return launch_direct<SC, KERNEL_TILE8>(F, slots, evals, s);
+}
+
 template <int SC>
 hipError_t launch_scene(const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
                         hipStream_t s) {

@@ -27,4 +27,11 @@ hipError_t launch_eval_og(const FrameConst& F, const float* pts, long long n, fl
     return launch_eval<SCENE_OG>(F, pts, n, dist, mat, s);
 }
 
+hipError_t launch_wire_o(const FrameConst& F, WireTile* slots, unsigned long long* evals, hipStream_t s) {
+    return launch_scene_wire<SCENE_O>(F, slots, evals, s);
+}
+hipError_t launch_wire_og(const FrameConst& F, WireTile* slots, unsigned long long* evals, hipStream_t s) {
+    return launch_scene_wire<SCENE_OG>(F, slots, evals, s);
+}
+
 }  // namespace rm

@@ -21,4 +21,11 @@ hipError_t launch_eval_t(const FrameConst& F, const float* pts, long long n, flo
     return launch_eval<SCENE_T>(F, pts, n, dist, mat, s);
 }
 
+hipError_t launch_wire_s0(const FrameConst& F, WireTile* slots, unsigned long long* evals, hipStream_t s) {
+    return launch_scene_wire<SCENE_S0>(F, slots, evals, s);
+}
+hipError_t launch_wire_t(const FrameConst& F, WireTile* slots, unsigned long long* evals, hipStream_t s) {
+    return launch_scene_wire<SCENE_T>(F, slots, evals, s);
+}
+
 }  // namespace rm

@@ -20,6 +20,11 @@ inline TileGrid tile_grid(int kernel, int W, int rows) {
 }
 
 // out: W-wide rows of float4 (rgba8 = false) or RGBA8 words (rgba8 = true)
+struct WireTile;
+// rm_render_cycle_rows_wire: the built-in scenes' render kernel (8x8 one-wave
+// tiles) encoding every tile into its wire slot instead of storing pixels
+hipError_t launch_render_wire(int scene, const FrameConst& F, WireTile* slots, unsigned long long* evals,
+                              hipStream_t s);
 hipError_t launch_render(int scene, const FrameConst& F, void* out, bool rgba8, unsigned long long* evals, int kernel,
                          hipStream_t s);
 // sceneSDF(p) of a compiled-in scene at n points (rm_scene_eval)
@@ -48,15 +53,14 @@ hipError_t launch_deinterleave_cycle_rgb8(const uint8_t* gathered, uint32_t* out
 // for the following launch
 hipError_t launch_tile_order(const uint32_t* cost, int n, int gx, int radius, uint32_t* order, uint32_t* hist,
                              uint32_t* next, uint8_t* bucket, hipStream_t s);
-// l3 (optional): FXAA's output also as mip level 3 (W/8 x H/8 exact-halving
-// texels, see BloomPlan::chain); only where chain_fxaa_ok(W, H)
-hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s, uint32_t* l3 = nullptr);
-bool chain_fxaa_ok(int W, int H);
+hipError_t launch_fxaa(const uint32_t* in, uint32_t* out, int W, int H, hipStream_t s);
 // rm_wire.hip: the compressed RGB wire of RGBA8 row parts
 long long wire_capacity(int W, int n);
 long long wire_workspace(int W, int n);
 hipError_t launch_wire_encode(const uint32_t* rows, int W, int n, uint8_t* msg, void* workspace,
                               long long* size_out, hipStream_t s);
+// the scan and compaction of slots already written (rm_wire_tile.h: a render epilogue, or the rows encoder)
+hipError_t launch_wire_finish(const void* workspace, int W, int n, uint8_t* msg, long long* size_out, hipStream_t s);
 hipError_t launch_wire_decode(const uint8_t* msg, int n, int W, int cycle, int offset, int run, uint32_t* frame,
                               hipStream_t s);
 constexpr int kMaxWireParts = 64;
@@ -85,18 +89,11 @@ struct BloomPlan {
     // polynomials (rm_post.hip).  All but the polynomials depend on W x H only.
     size_t base_ent[2] = {}, run_ent[4] = {}, run_tup[4] = {}, run_count = 0, poly_tab[2] = {};
     int nruns[4] = {};  // most runs an axis can have
-    // rm_post_chain (FXAA then bloom of its output): the FXAA kernel writes mip
-    // level 3 of its output from registers (8x8-pixel blocks, mip_mean4 chain)
-    // and the pyramid starts there, instead of re-reading the frame: set when
-    // levels 4..d2 are 5 to 8 exact halvings of level 3 (launch_bloom's
-    // pyramid kernel) and the FXAA kernel's blocks tile the frame
-    bool chain = false;
 };
 BloomPlan bloom_plan(int W, int H);
 // runs_cached: the buffer already holds this W x H's run tables, written on
 // this stream (only the mip levels and the polynomials are rebuilt)
-// from_l3 (p.chain): mips + p.offset[3] already holds level 3 of `in`
 hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s,
-                        bool runs_cached, bool from_l3 = false);
+                        bool runs_cached);
 
 }  // namespace rm

@@ -350,7 +350,10 @@ __global__ __launch_bounds__(256) void rm_bloom_poly_kernel(BloomAxes axes, Bloo
     dst[2] = make_float4((float)(P[8] * lam), (float)(P[9] * lam), (float)(P[10] * lam), (float)(P[11] * lam));
 }
 
-constexpr int kBloomRows = 16;
+#ifndef RM_BLOOM_ROWS
+#define RM_BLOOM_ROWS 16
+#endif
+constexpr int kBloomRows = RM_BLOOM_ROWS;
 template <typename T>
 __device__ __forceinline__ T sload_entry(const T* base, int i) {  // a wave-uniform 8-byte entry via the scalar cache
     static_assert(sizeof(T) == 8, "8-byte entries");
@@ -402,7 +405,10 @@ __device__ __forceinline__ RGB base_bilinear(const uint32_t* r0, const uint32_t*
 // One lane per column of a kBloomRows strip, the rows in batches of
 // kBloomBatch whose texel loads are issued together (the loads in flight per
 // wave, not the arithmetic, bound a lone strip).
-constexpr int kBloomBatch = 8;
+#ifndef RM_BLOOM_BATCH
+#define RM_BLOOM_BATCH 8
+#endif
+constexpr int kBloomBatch = RM_BLOOM_BATCH;
 __global__ __launch_bounds__(256) void rm_bloom_min_kernel(const uint32_t* __restrict__ in, BloomPix B,
                                                            uint32_t* __restrict__ out, int W, int H) {
     const int x = blockIdx.x * 256 + threadIdx.x;
@@ -477,8 +483,6 @@ BloomPlan bloom_plan(int W, int H) {
         p.d2 = p.d1 + 1 > q ? q : p.d1 + 1;
     }
     p.fr = p.lod - floorf(p.lod);
-    const long long T2c = 1LL << (p.d2 < 62 ? p.d2 : 62);
-    p.chain = p.lod > 0.0f && p.d2 - 3 >= 5 && p.d2 - 3 <= 8 && W % T2c == 0 && H % T2c == 0 && chain_fxaa_ok(W, H);
     int w = W, h = H;
     p.w[0] = W;
     p.h[0] = H;
@@ -520,22 +524,18 @@ BloomPlan bloom_plan(int W, int H) {
 }
 
 hipError_t launch_bloom(const uint32_t* in, uint32_t* out, uint32_t* mips, const BloomPlan& p, hipStream_t s,
-                        bool runs_cached, bool from_l3) {
+                        bool runs_cached) {
     const int W = p.w[0], H = p.h[0];
     if (W <= 0 || H <= 0) return hipSuccess;
-    if (from_l3 && !p.chain) return hipErrorInvalidValue;
     const uint32_t* lv[40] = {in};
     // levels 1..d2: when W and H are multiples of 2^d2 every level is an exact
     // halving, and the last 5..8 levels come from one rm_mip_pyramid_kernel
     // launch over level s = max(d2 - 8, 0) (only d1, d2 written); otherwise,
     // and for levels 1..s, one rm_mip_down_kernel launch per level
-    // (from_l3: level 3 is in the buffer, written by the FXAA kernel of rm_post_chain, and the pyramid
-    // starts there)
     const long long T2 = 1LL << (p.d2 < 62 ? p.d2 : 62);
-    const int s0 = from_l3 ? 3 : p.d2 > 8 ? p.d2 - 8 : 0;
+    const int s0 = p.d2 > 8 ? p.d2 - 8 : 0;
     const bool pyramid = p.lod > 0.0f && p.d2 - s0 >= 5 && W % T2 == 0 && H % T2 == 0;
-    if (from_l3) lv[3] = mips + p.offset[3];
-    for (int k = from_l3 ? 4 : 1; k <= (pyramid ? s0 : p.d2); k++) {
+    for (int k = 1; k <= (pyramid ? s0 : p.d2); k++) {
         uint32_t* dst = mips + p.offset[k];
         const int w = p.w[k - 1], h = p.h[k - 1], w1 = p.w[k], h1 = p.h[k];
         hipLaunchKernelGGL(rm_mip_down_kernel, dim3((w1 + 15) / 16, (h1 + 15) / 16), dim3(256), 0, s, lv[k - 1], dst,

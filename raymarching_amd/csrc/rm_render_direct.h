@@ -7,6 +7,7 @@
 // wave-compacted state machine would not pay for its phase switching.
 #pragma once
 #include "rm_device.h"
+#include "rm_wire_tile.h"
 
 namespace rm {
 
@@ -987,6 +988,12 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
     }
     const int x = bx * T::TW + (w & 1) * 8 + (lane % T::LW);
     const int j = by * T::TH + (w >> 1) * 8 + (lane / T::LW);
+    // OUT = WireTile (rm_render_cycle_rows_wire): the wave's 8x8 tile is not
+    // stored as pixels but encoded for the compressed wire from registers
+    // (rm_wire_tile.h) into the workspace, tile by * gx + bx of the part
+    constexpr bool kWire = IsWireTile<OUT>::value;
+    static_assert(!kWire || (T::WPB == 1 && T::TW == 8 && T::TH == 8), "the wire codes one 8x8 wave tile");
+    uint32_t wire_px = 0;  // (kWire: this lane's RGBA8 word, 0 outside the part)
     Tally cnt;
     if (x < F.W && j < F.nrows) {
         const int y = shard_row(F, F.row0 + j);
@@ -1006,8 +1013,12 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
             c = render_pixel<SC, 3, kPlaneSpans<SC> ? (COUNT ? 2 : 1) : 0>(F, ro, rd, cnt);
         }
         c = post_colour<FastColour<SC>::value>(c, vig);
-        store_pixel(F, out, (size_t)j * F.W + x, c);
+        if constexpr (kWire) wire_px = pack_rgba8(c.x, c.y, c.z, 1.0f);
+        else store_pixel(F, out, (size_t)j * F.W + x, c);
     }
+    if constexpr (kWire)
+        wire_encode_tile(wire_px, reinterpret_cast<WireTile*>(out), (long long)gx * ((F.nrows + 7) / 8),
+                         (long long)by * gx + bx);
     if (T::WPB == 1 && F.tile_cost && lane == 0) {  // this tile's duration: the next launch's dispatch order
         const uint64_t dt = clock64() - t_start;
         F.tile_cost[by * gx + bx] = dt > 0xffffffffull ? 0xffffffffu : (uint32_t)dt;

@@ -1,103 +1,65 @@
 // rm_wire.hip -- a lossless compressed wire for RGBA8 row parts (multi-GPU
-// frames).  The frames the pass renders are smooth along rows
-// (sky gradients, flat floor and sponge faces), so each 64-pixel row segment
-// -- one wave's store -- is sent as its first pixel plus the left differences
-// of the other 63, per channel, at the segment's bit width:
+// frames): the per-tile code of rm_wire_tile.h, whose message
+// layout it also describes.  The frames the pass renders are smooth along rows
+// and columns (sky gradients, flat floor and sponge faces), so an 8x8 tile
+// costs a header and a few bit planes instead of 192 B of RGB8.
 //
-//   d = (p[l] - p[l-1]) mod 256 as int8, z = zig-zag(d) in 0..255,
-//   b_c = bit width of max_l z_c (0..8), and bit i of z_c over the 64 lanes is
-//   one 64-bit word (a wave ballot; lane 0 contributes 0).
-//
-// A segment costs 8 B of header (first pixel's RGB, three widths) plus
-// 8 B per bit plane, against 192 B as RGB8; flat segments cost 8 B.  Alpha is
-// not sent (the pass writes 1: the root stores 255, as the RGB8 wire does).
-//
-// Message of a part of n packed rows, W pixels, S = ceil(W / 64) segments:
-//   [0, 8)            uint64 message bytes
-//   [8, 8 + 4n)       uint32 row offset of each row's words in the payload
-//   then n * S bytes  words per segment (1 + planes), padded to 8 B
-//   then payload      uint64 words: per row, per segment: header, planes
-// The encoder writes every segment's words into a fixed slot of a workspace
-// (25 words: the widest segment), then scans the rows and compacts the slots
-// into the message; the decoder gives every segment a wave, which sums the
-// row's earlier segment sizes and rebuilds its 64 pixels with a wave-wide
-// prefix sum of the differences.
+// Encoding is three steps: every tile's words into a fixed slot of a
+// workspace (kTileWords words; rm_wire_tile_rows here from RGBA8 rows, or the
+// render kernel's own epilogue, rm_render_cycle_rows_wire, which never writes
+// the rows), one workgroup scanning the tiles' word counts into the message's
+// offset table, and the slots compacted into the payload.  The decoder gives
+// every tile a wave, which reads its offset, rebuilds the 64 differences from
+// the planes and sums them along the tile's rows and its first column.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "rm_launch.h"
+#include "rm_wire_tile.h"
 
 namespace rm {
 
-constexpr int kSegWords = 25;  // header + 3 x 8 planes
+__device__ __forceinline__ size_t wire_header_bytes(long long T) { return 8 + (((size_t)4 * T + 7) & ~(size_t)7); }
+__host__ __device__ inline long long wire_chunks(long long T) { return (T + 63) / 64; }
+__host__ __device__ inline long long wire_bases_offset(long long T) { return (wire_counts_offset(T) + T + 3) & ~3ll; }
 
-__device__ __forceinline__ uint32_t zigzag8(int d) {  // d in -255..255 -> the int8 wrap, zig-zagged
-    const int s = (int)(int8_t)(uint8_t)(d & 255);
-    return (uint32_t)(s >= 0 ? 2 * s : -2 * s - 1);
-}
-__device__ __forceinline__ int unzigzag8(uint32_t z) { return (int)(z >> 1) ^ -(int)(z & 1u); }
-
-__device__ __forceinline__ uint64_t ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-
-// bit width of the wave maximum of z (0..8), wave-uniform
-__device__ __forceinline__ int wave_width(uint32_t z) {
-    int b = 0;
-    for (int i = 7; i >= 0; i--)
-        if (ballot64((z >> i) & 1u)) {
-            b = i + 1;
-            break;
-        }
-    return b;
+// E1 from RGBA8 rows: one wave per tile (grid TX x TY)
+__global__ __launch_bounds__(64) void rm_wire_tile_rows(const uint32_t* __restrict__ rows, int W, int n,
+                                                        WireTile* __restrict__ ws) {
+    const int tx = blockIdx.x, ty = blockIdx.y, l = threadIdx.x;
+    const int x = tx * 8 + (l & 7), y = ty * 8 + (l >> 3);
+    const uint32_t p = x < W && y < n ? rows[(size_t)y * W + x] : 0u;
+    wire_encode_tile(p, ws, (long long)gridDim.x * gridDim.y, (long long)ty * gridDim.x + tx);
 }
 
-// E1: one wave per segment (grid S x n, 64 threads): its words into the slot,
-// its word count into the message's count table, the row's total (atomics).
-__global__ __launch_bounds__(64) void rm_wire_seg_encode(const uint32_t* __restrict__ rows, int W, int n,
-                                                         uint64_t* __restrict__ slots, uint8_t* __restrict__ counts,
-                                                         uint32_t* __restrict__ row_words) {
-    const int k = blockIdx.x, j = blockIdx.y, l = threadIdx.x, S = gridDim.x;
-    const int x = k * 64 + l;
-    const uint32_t p = rows[(size_t)j * W + (x < W ? x : W - 1)];  // past the row end: repeats the last pixel
-    const uint32_t left = __shfl(p, l > 0 ? l - 1 : 0, 64);
-    uint32_t z[3];
-    int b[3], total = 0;
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-        z[c] = l == 0 ? 0u : zigzag8((int)((p >> (8 * c)) & 255u) - (int)((left >> (8 * c)) & 255u));
-        b[c] = wave_width(z[c]);
-        total += b[c];
-    }
-    // lane 0: the header; lane q + 1: plane q (channel-major, low bit first)
-    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)p) & 0xFFFFFFu;
-    uint64_t v = (uint64_t)first | ((uint64_t)b[0] << 24) | ((uint64_t)b[1] << 28) | ((uint64_t)b[2] << 32);
-    int q = 1;
-#pragma unroll
-    for (int c = 0; c < 3; c++)
-        for (int i = 0; i < b[c]; i++, q++) {
-            const uint64_t plane = ballot64((z[c] >> i) & 1u);
-            if (l == q) v = plane;
-        }
-    const size_t seg = (size_t)j * S + k;
-    if (l <= total) slots[seg * kSegWords + l] = v;
-    if (l == 0) {
-        counts[seg] = (uint8_t)(1 + total);
-        atomicAdd(&row_words[j], (uint32_t)(1 + total));
-    }
-}
-
-__device__ __forceinline__ size_t wire_header_bytes(int n, int S) {
-    return 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (((size_t)n * S + 7) & ~(size_t)7);
-}
-
-// E2: one workgroup: exclusive scan of the rows' word counts into the
-// message's row offsets; the message size into the message and *size_out.
-__global__ __launch_bounds__(1024) void rm_wire_row_scan(const uint32_t* __restrict__ row_words, int n, int S,
+// E2: one workgroup: the word counts of each 64-tile chunk (16 counts per
+// 16-byte load), an exclusive scan of the chunks into their bases (in the
+// workspace), the message size into the message and *size_out
+__global__ __launch_bounds__(1024) void rm_wire_tile_scan(const uint8_t* __restrict__ ws, long long T,
                                                           uint8_t* __restrict__ msg, long long* __restrict__ size_out) {
     __shared__ unsigned long long part[1024];
     const int t = threadIdx.x;
-    const int per = (n + 1023) / 1024, j0 = t * per, j1 = min(n, j0 + per);
+    const uint8_t* counts = ws + wire_counts_offset(T);
+    uint32_t* bases = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(ws) + wire_bases_offset(T));
+    const long long C = wire_chunks(T), per = (C + 1023) / 1024, c0 = t * per, c1 = c0 + per < C ? c0 + per : C;
+    auto chunk_sum = [&](long long c) {
+        const long long i0 = c * 64, i1 = i0 + 64 < T ? i0 + 64 : T;
+        uint32_t s = 0;
+        if (i1 - i0 == 64 && ((reinterpret_cast<uintptr_t>(counts) + i0) & 15) == 0) {
+            const uint4* q = reinterpret_cast<const uint4*>(counts + i0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint4 v = q[k];
+                for (uint32_t w : {v.x, v.y, v.z, v.w})  // four counts per word, each < 256
+                    s += (w & 255u) + ((w >> 8) & 255u) + ((w >> 16) & 255u) + (w >> 24);
+            }
+        } else {
+            for (long long i = i0; i < i1; i++) s += counts[i];
+        }
+        return s;
+    };
     unsigned long long s = 0;
-    for (int j = j0; j < j1; j++) s += row_words[j];
+    for (long long c = c0; c < c1; c++) s += chunk_sum(c);
     part[t] = s;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the thread sums
@@ -107,127 +69,150 @@ __global__ __launch_bounds__(1024) void rm_wire_row_scan(const uint32_t* __restr
         __syncthreads();
     }
     unsigned long long off = t > 0 ? part[t - 1] : 0ull;
-    uint32_t* row_off = reinterpret_cast<uint32_t*>(msg + 8);
-    for (int j = j0; j < j1; j++) {
-        row_off[j] = (uint32_t)off;
-        off += row_words[j];
+    for (long long c = c0; c < c1; c++) {
+        bases[c] = (uint32_t)off;
+        off += chunk_sum(c);
     }
     if (t == 1023) {
-        const long long bytes = (long long)wire_header_bytes(n, S) + 8ll * (long long)part[1023];
+        const long long bytes = (long long)wire_header_bytes(T) + 8ll * (long long)part[1023];
         *reinterpret_cast<long long*>(msg) = bytes;
         if (size_out) *size_out = bytes;
     }
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+// E3: one wave per 64-tile chunk, lane = tile: its offset (the chunk's base
+// plus a wave scan of the counts) into the table, its words into the payload
+// (word q of the chunk's tiles: one coalesced load)
+__global__ __launch_bounds__(256) void rm_wire_tile_compact(const uint8_t* __restrict__ ws, long long T,
+                                                            uint8_t* __restrict__ msg) {
+    const long long chunk = 4ll * blockIdx.x + (threadIdx.x >> 6);  // (four 64-tile chunks per workgroup)
+    const long long t = 64ll * chunk + (threadIdx.x & 63);
+    const int l = threadIdx.x & 63;
+    if (chunk >= wire_chunks(T)) return;  // (wave-uniform)
+    const uint32_t base = reinterpret_cast<const uint32_t*>(ws + wire_bases_offset(T))[chunk];
+    const uint32_t cnt = t < T ? ws[wire_counts_offset(T) + t] : 0u;
+    uint32_t x = cnt;  // inclusive scan over the lanes
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// words of a row's segments before segment k (one wave, wave-uniform result)
-__device__ __forceinline__ uint32_t seg_offset(const uint8_t* __restrict__ counts, int k, int l) {
-    uint32_t acc = 0;
-    for (int c0 = 0; c0 < k; c0 += 64) {
-        const int kk = c0 + l;
-        acc += wave_sum(kk < k ? (uint32_t)counts[kk] : 0u);
+    for (int k = 1; k < 64; k <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)x, k, 64);
+        if (l >= k) x += u;
     }
-    return acc;
+    const uint32_t off = base + x - cnt;
+    if (t >= T) return;
+    reinterpret_cast<uint32_t*>(msg + 8)[t] = off << 5 | cnt;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(ws);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(msg + wire_header_bytes(T)) + off;
+    // (eight words' loads in flight before their stores; most tiles have fewer)
+    for (uint32_t q0 = 0; q0 < cnt; q0 += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) v[k] = q0 + k < cnt ? src[(q0 + k) * T + t] : 0ull;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++)
+            if (q0 + k < cnt) dst[q0 + k] = v[k];
+    }
 }
 
-// E3: one wave per segment (grid S x n): its slot's words into the payload
-__global__ __launch_bounds__(64) void rm_wire_compact(const uint64_t* __restrict__ slots, int n,
-                                                      uint8_t* __restrict__ msg) {
-    const int k = blockIdx.x, j = blockIdx.y, l = threadIdx.x, S = gridDim.x;
-    const size_t hb = wire_header_bytes(n, S);
-    const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
-    const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
-    const int cnt = counts[k];
-    if (l < cnt)
-        reinterpret_cast<uint64_t*>(msg + hb)[off + l] = slots[((size_t)j * S + k) * kSegWords + l];
+// D: a wave rebuilds 8 tiles (tx0 .. tx0 + 7 of tile row ty) of a part into
+// their pixels of the frame (the part's packed row j is frame row y(j): (y mod
+// cycle) - offset in [0, run)).  The 8 table entries and then every tile's
+// words are loaded before any is decoded (two memory round trips for the 8).
+// Lane l = pixel (l & 7, l >> 3) of a tile.
+//
+// Per tile, cross-lane work only on the VALU (no LDS): a bit plane is a
+// 64-bit lane mask, so lane l's bit is one v_cndmask with the plane in an SGPR
+// pair; the differences are summed along each row of 8 lanes (DPP row_shr by
+// 1, 2, 4: the sources of a shift are zeroed where they would cross into the
+// next row of the tile, and row_shr:4 skips the first half of each 8-lane row
+// by its bank mask) and the first column's differences down the tile (a
+// wave-wide inclusive scan of the first-column lanes: row_shr 1, 2, 4, 8,
+// row_bcast:15, row_bcast:31), whose sum at any lane of tile row r is that
+// row's first pixel.
+__device__ __forceinline__ uint32_t lane_bit(uint64_t plane) {  // bit l of a wave-uniform 64-bit word
+    uint32_t r;
+    asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(r) : "s"(plane));
+    return r;
 }
-
-// D: one wave per segment of a part's packed row j (grid S x n): rebuilt into
-// frame row y(j) (the part's rows: (y mod cycle) - offset in [0, run))
-__global__ __launch_bounds__(64) void rm_wire_decode(const uint8_t* __restrict__ msg, int n, int W, int cycle,
-                                                     int offset, int run, uint32_t* __restrict__ frame) {
-    const int k = blockIdx.x, j = blockIdx.y, l = threadIdx.x, S = gridDim.x;
-    const size_t hb = wire_header_bytes(n, S);
-    const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
-    const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
-    const int cnt = min((int)counts[k], kSegWords);  // (a corrupt count cannot read past the segment)
-    const uint64_t* sw = reinterpret_cast<const uint64_t*>(msg + hb) + off;
-    const uint64_t mine = l < cnt ? sw[l] : 0ull;  // lane 0: header, lane q + 1: plane q
-    const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
-    const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_lo);
-    const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_hi);
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // DPP move; disabled and out-of-row lanes read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, BANK_MASK, true);
+}
+__device__ __forceinline__ uint32_t wire_decode_tile(uint64_t mine, int l) {
+    const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mine);
+    const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mine >> 32));
     const int b[3] = {min((int)((h_lo >> 24) & 15u), 8), min((int)(h_lo >> 28), 8), min((int)(h_hi & 15u), 8)};
-    // this lane's bit of a plane word: from the low half for lanes 0-31, the high half for 32-63
-    const uint32_t sh = (uint32_t)(l & 31);
-    const bool hi_half = l >= 32;
-    uint32_t px = 0;
+    const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
+    uint32_t d[3];
     int q = 1;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         uint32_t z = 0;
         for (int i = 0; i < b[c]; i++, q++) {
-            const uint32_t w = hi_half ? (uint32_t)__builtin_amdgcn_readlane((int)m_hi, q)
-                                       : (uint32_t)__builtin_amdgcn_readlane((int)m_lo, q);
-            z |= ((w >> sh) & 1u) << i;
+            const uint64_t plane = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m_lo, q) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m_hi, q) << 32);
+            z |= lane_bit(plane) << i;
         }
-        int d = l == 0 ? (int)((h_lo >> (8 * c)) & 255u) : unzigzag8(z);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {  // inclusive prefix sum over the lanes
-            const int u = __shfl_up(d, o, 64);
-            if (l >= o) d += u;
-        }
-        px |= (uint32_t)(d & 255) << (8 * c);
+        const int s = (int)(z >> 1) ^ -(int)(z & 1u);  // zig-zag back: the difference as int8
+        d[c] = l == 0 ? (h_lo >> (8 * c)) & 255u : (uint32_t)s & 255u;
     }
-    const int c0 = j / run, y = c0 * cycle + offset + (j - c0 * run);
-    const int x = k * 64 + l;
-    if (x < W) frame[(size_t)y * W + x] = px | 0xFF000000u;
+    // the sums mod 256 per channel, two channels per word in 16-bit fields (at
+    // most 64 x 255 < 2^16: no carry between fields)
+    const int c8 = l & 7;
+    const uint32_t A = d[0] | (d[1] << 16), B = d[2];
+    // first column: the inclusive wave scan of its lanes (other lanes 0)
+    uint32_t ya = c8 == 0 ? A : 0u, yb = c8 == 0 ? B : 0u;
+    ya += dpp0<0x111>(ya), yb += dpp0<0x111>(yb);  // row_shr:1
+    ya += dpp0<0x112>(ya), yb += dpp0<0x112>(yb);  // row_shr:2
+    ya += dpp0<0x114>(ya), yb += dpp0<0x114>(yb);  // row_shr:4
+    ya += dpp0<0x118>(ya), yb += dpp0<0x118>(yb);  // row_shr:8
+    ya += dpp0<0x142, 0xa>(ya), yb += dpp0<0x142, 0xa>(yb);  // row_bcast:15 into rows 1, 3
+    ya += dpp0<0x143, 0xc>(ya), yb += dpp0<0x143, 0xc>(yb);  // row_bcast:31 into rows 2, 3
+    // along each tile row: the other columns' differences, scanned in 8-lane segments
+    uint32_t xa = c8 == 0 ? 0u : A, xb = c8 == 0 ? 0u : B;
+    xa += dpp0<0x111>(c8 == 7 ? 0u : xa), xb += dpp0<0x111>(c8 == 7 ? 0u : xb);  // (no source across a row end)
+    xa += dpp0<0x112>(c8 >= 6 ? 0u : xa), xb += dpp0<0x112>(c8 >= 6 ? 0u : xb);
+    xa += dpp0<0x114, 0xf, 0xa>(xa), xb += dpp0<0x114, 0xf, 0xa>(xb);  // (banks 1, 3: lanes c8 >= 4)
+    const uint32_t va = xa + ya, vb = xb + yb;
+    return (va & 255u) | (((va >> 16) & 255u) << 8) | ((vb & 255u) << 16) | 0xFF000000u;
 }
 
-// D for several parts in one launch (grid S x max rows x parts)
-__global__ __launch_bounds__(64) void rm_wire_decode_parts(WireParts parts, int W, uint32_t* __restrict__ frame) {
-    const WirePart& P = parts.part[blockIdx.z];
-    const int k = blockIdx.x, l = threadIdx.x, S = gridDim.x, n = P.nrows;
-    const size_t hb = wire_header_bytes(n, S);
-    for (int j = blockIdx.y; j < n; j += gridDim.y) {
-        const uint8_t* msg = P.msg;
-        const uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7) + (size_t)j * S;
-        const uint32_t off = reinterpret_cast<const uint32_t*>(msg + 8)[j] + seg_offset(counts, k, l);
-        const int cnt = min((int)counts[k], kSegWords);
-        const uint64_t* sw = reinterpret_cast<const uint64_t*>(msg + hb) + off;
-        const uint64_t mine = l < cnt ? sw[l] : 0ull;
-        const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
-        const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_lo);
-        const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m_hi);
-        const int b[3] = {min((int)((h_lo >> 24) & 15u), 8), min((int)(h_lo >> 28), 8), min((int)(h_hi & 15u), 8)};
-        const uint32_t sh = (uint32_t)(l & 31);
-        const bool hi_half = l >= 32;
-        uint32_t px = 0;
-        int q = 1;
+constexpr int kDecodeTiles = 8;  // tiles per wave
+constexpr int kDecodeWaves = 4;  // waves per workgroup (one-wave workgroups cap a CU's resident waves)
+__device__ __forceinline__ void wire_decode_tiles(const uint8_t* __restrict__ msg, int n, int W, int tx0, int ty,
+                                                  int cycle, int offset, int run, uint32_t* __restrict__ frame) {
+    const int l = threadIdx.x & 63, TX = (W + 7) / 8;
+    if (tx0 >= TX) return;  // (wave-uniform)
+    const long long T = (long long)TX * ((n + 7) / 8), t0 = (long long)ty * TX + tx0;
+    const int nt = TX - tx0 < kDecodeTiles ? TX - tx0 : kDecodeTiles;
+    const uint32_t ent = l < nt ? reinterpret_cast<const uint32_t*>(msg + 8)[t0 + l] : 0u;
+    const uint64_t* payload = reinterpret_cast<const uint64_t*>(msg + wire_header_bytes(T));
+    uint64_t mine[kDecodeTiles];
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            uint32_t z = 0;
-            for (int i = 0; i < b[c]; i++, q++) {
-                const uint32_t w = hi_half ? (uint32_t)__builtin_amdgcn_readlane((int)m_hi, q)
-                                           : (uint32_t)__builtin_amdgcn_readlane((int)m_lo, q);
-                z |= ((w >> sh) & 1u) << i;
-            }
-            int d = l == 0 ? (int)((h_lo >> (8 * c)) & 255u) : unzigzag8(z);
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int u = __shfl_up(d, o, 64);
-                if (l >= o) d += u;
-            }
-            px |= (uint32_t)(d & 255) << (8 * c);
-        }
-        const int c0 = j / P.run, y = c0 * parts.cycle + P.offset + (j - c0 * P.run);
-        const int x = k * 64 + l;
-        if (x < W) frame[(size_t)y * W + x] = px | 0xFF000000u;
+    for (int k = 0; k < kDecodeTiles; k++) {
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)ent, k);
+        const uint32_t cnt = min(e & 31u, (uint32_t)kTileWords);  // (a corrupt count cannot read past the tile)
+        mine[k] = k < nt && (uint32_t)l < cnt ? payload[(e >> 5) + l] : 0ull;
     }
+    const int j = ty * 8 + (l >> 3);
+    const int c0 = j / run, y = c0 * cycle + offset + (j - c0 * run);
+#pragma unroll
+    for (int k = 0; k < kDecodeTiles; k++) {
+        if (k >= nt) break;
+        const uint32_t px = wire_decode_tile(mine[k], l);
+        const int x = (tx0 + k) * 8 + (l & 7);
+        if (x < W && j < n) frame[(size_t)y * W + x] = px;
+    }
+}
+
+// D for several parts in one launch (grid ceil(TX / 32) x tile rows x parts,
+// wave w of a workgroup: tiles 8 (4 x + w) .. + 7 of the row)
+__global__ __launch_bounds__(64 * kDecodeWaves) void rm_wire_tile_decode_parts(WireParts parts, int W,
+                                                                               uint32_t* __restrict__ frame) {
+    const WirePart& P = parts.part[blockIdx.z];
+    const int TY = (P.nrows + 7) / 8;
+    const int tx0 = (blockIdx.x * kDecodeWaves + (threadIdx.x >> 6)) * kDecodeTiles;
+    for (int ty = blockIdx.y; ty < TY; ty += gridDim.y)
+        wire_decode_tiles(P.msg, P.nrows, W, tx0, ty, parts.cycle, P.offset, P.run, frame);
 }
 
 // a part's packed RGBA8 rows into their frame rows (the root's own part)
@@ -242,48 +227,54 @@ __global__ __launch_bounds__(256) void rm_scatter_part(const uint32_t* __restric
 }
 
 long long wire_capacity(int W, int n) {
-    const long long S = (W + 63) / 64;
-    return 8 + ((4ll * n + 7) & ~7ll) + ((n * S + 7) & ~7ll) + 8ll * kSegWords * n * S;
+    const long long T = (long long)((W + 7) / 8) * ((n + 7) / 8);
+    return 8 + ((4 * T + 7) & ~7ll) + 8ll * kTileWords * T;
 }
 
 long long wire_workspace(int W, int n) {
-    const long long S = (W + 63) / 64;
-    return 8ll * kSegWords * n * S + 4ll * n;
+    const long long T = (long long)((W + 7) / 8) * ((n + 7) / 8);
+    return wire_bases_offset(T) + 4 * wire_chunks(T);
+}
+
+// E2 + E3 over a workspace already written (by rm_wire_tile_rows or a render epilogue)
+hipError_t launch_wire_finish(const void* workspace, int W, int n, uint8_t* msg, long long* size_out, hipStream_t s) {
+    const long long T = (long long)((W + 7) / 8) * ((n + 7) / 8);
+    const uint8_t* ws = reinterpret_cast<const uint8_t*>(workspace);
+    hipLaunchKernelGGL(rm_wire_tile_scan, dim3(1), dim3(1024), 0, s, ws, T, msg, size_out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || T == 0) return e;
+    hipLaunchKernelGGL(rm_wire_tile_compact, dim3((unsigned)((wire_chunks(T) + 3) / 4)), dim3(256), 0, s, ws, T, msg);
+    return hipGetLastError();
 }
 
 hipError_t launch_wire_encode(const uint32_t* rows, int W, int n, uint8_t* msg, void* workspace,
                               long long* size_out, hipStream_t s) {
-    const int S = (W + 63) / 64;
-    uint64_t* slots = reinterpret_cast<uint64_t*>(workspace);
-    uint32_t* row_words = reinterpret_cast<uint32_t*>(slots + (size_t)kSegWords * n * S);
-    uint8_t* counts = msg + 8 + (((size_t)4 * n + 7) & ~(size_t)7);
-    hipError_t e = hipMemsetAsync(row_words, 0, (size_t)4 * n, s);
-    if (e != hipSuccess) return e;
     if (n > 0) {
-        hipLaunchKernelGGL(rm_wire_seg_encode, dim3(S, n), dim3(64), 0, s, rows, W, n, slots, counts, row_words);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(rm_wire_tile_rows, dim3((W + 7) / 8, (n + 7) / 8), dim3(64), 0, s, rows, W, n,
+                           reinterpret_cast<WireTile*>(workspace));
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(rm_wire_row_scan, dim3(1), dim3(1024), 0, s, row_words, n, S, msg, size_out);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (n > 0) hipLaunchKernelGGL(rm_wire_compact, dim3(S, n), dim3(64), 0, s, slots, n, msg);
-    return hipGetLastError();
+    return launch_wire_finish(workspace, W, n, msg, size_out, s);
 }
 
 hipError_t launch_wire_decode(const uint8_t* msg, int n, int W, int cycle, int offset, int run, uint32_t* frame,
                               hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const int S = (W + 63) / 64;
-    hipLaunchKernelGGL(rm_wire_decode, dim3(S, n), dim3(64), 0, s, msg, n, W, cycle, offset, run, frame);
-    return hipGetLastError();
+    WireParts parts{};
+    parts.n = 1;
+    parts.cycle = cycle;
+    parts.part[0] = WirePart{msg, n, offset, run};
+    return launch_wire_decode_parts(parts, W, frame, s);
 }
 
 hipError_t launch_wire_decode_parts(const WireParts& parts, int W, uint32_t* frame, hipStream_t s) {
     int rows = 0;
     for (int i = 0; i < parts.n; i++) rows = parts.part[i].nrows > rows ? parts.part[i].nrows : rows;
     if (parts.n <= 0 || rows <= 0) return hipSuccess;
-    const int S = (W + 63) / 64;
-    hipLaunchKernelGGL(rm_wire_decode_parts, dim3(S, rows < 65535 ? rows : 65535, parts.n), dim3(64), 0, s, parts,
-                       W, frame);
+    const int TY = (rows + 7) / 8;
+    const int per = kDecodeTiles * kDecodeWaves, gx = ((W + 7) / 8 + per - 1) / per;
+    hipLaunchKernelGGL(rm_wire_tile_decode_parts, dim3(gx, TY < 65535 ? TY : 65535, parts.n), dim3(64 * kDecodeWaves), 0,
+                       s, parts, W, frame);
     return hipGetLastError();
 }
 

@@ -588,6 +588,7 @@ class DeltaFrame(DistributedFrame):
         self.k = 0
         self.pending = None
         self.last_sizes = [0] * world
+        self.fused = rank != 0  # (the render kernel encodes; scene plugins fall back, _render_message)
         # the per-frame native calls with their arguments built once (a frame
         # at N = 8 is ~0.1 ms: Python-side argument checks per call would cost
         # as much as the GPU work)
@@ -612,6 +613,32 @@ class DeltaFrame(DistributedFrame):
                                           self.msg[slot].data_ptr(), self.ws[slot].data_ptr(),
                                           self.size_dev[slot].data_ptr()))
 
+    def _render_message(self, slot, stats=False):
+        """A non-root rank's part straight into its message: the render
+        kernel encodes its tiles in its epilogue (rm_render_cycle_rows_wire);
+        a scene plugin's part is rendered to rows and encoded after."""
+        import ctypes
+
+        from ._lib import RmError, RmStats
+        p, q = self.plan, self.rank
+        if self.fused:
+            s = RmStats()
+            try:
+                self._call(self._L.rm_render_cycle_rows_wire(
+                    self.r._ctx, p.W, p.H, p.cycle, p.offsets[q], p.part_runs[q], 0, self.nmine,
+                    self.msg[slot].data_ptr(), self.ws[slot].data_ptr(), self.size_dev[slot].data_ptr(),
+                    ctypes.byref(s) if stats else None))
+                return s.as_dict() if stats else None
+            except RmError as e:
+                if "built-in scenes only" not in str(e):
+                    raise
+                self.fused = False  # (a scene plugin: the two calls below from now on)
+        st = None
+        if self.nmine:
+            st = self._render_into(self.locals[slot], 0, self.nmine, stats=stats)
+        self._encode(slot)
+        return st[1] if stats and st is not None else None
+
     def _scatter(self, slot):
         p = self.plan
         self._call(self._L.rm_scatter_part_rgba8(self.r._ctx, p.W, p.H, p.cycle, p.offsets[0], p.part_runs[0],
@@ -630,14 +657,16 @@ class DeltaFrame(DistributedFrame):
             self.slot_works[slot] = []
             if events is not None:
                 events[0].record()
-            if self.nmine:
-                self._render_into(self.locals[slot], 0, self.nmine)
-            if events is not None:
-                events[1].record()
             if self.rank == 0:
+                if self.nmine:
+                    self._render_into(self.locals[slot], 0, self.nmine)
+                if events is not None:
+                    events[1].record()
                 self._scatter(slot)
             else:
-                self._encode(slot)
+                self._render_message(slot)  # (render and encode: one kernel plus the scan and compaction)
+                if events is not None:
+                    events[1].record()
                 self.size_host[slot].copy_(self.size_dev[slot], non_blocking=True)
                 self.size_ev[slot].record(st)
         self.r.set_stream(self.caller)
@@ -748,12 +777,18 @@ class DeltaFrame(DistributedFrame):
         return self.frame
 
     def render_local(self, stats=False):
+        """This rank's part once (rank 0: its rows; the others: their message,
+        as the frames make it); with stats, (rows or message, rm_stats)."""
         import torch
         st = self.streams[0]
         with torch.cuda.stream(st):
             self._bind(st)
             try:
-                res = self._render_into(self.locals[0], 0, self.nmine, stats=stats)
+                if self.rank == 0:
+                    res = self._render_into(self.locals[0], 0, self.nmine, stats=stats)
+                else:
+                    s = self._render_message(0, stats=stats)
+                    res = (self.msg[0], s) if stats else self.msg[0]
             finally:
                 self.r.set_stream(self.caller)
         if st is not self.caller:
@@ -776,13 +811,15 @@ class DeltaFrame(DistributedFrame):
         with torch.cuda.stream(st):
             self._bind(st)
             ev[0].record(st)
-            if self.nmine:
-                self._render_into(self.locals[slot], 0, self.nmine)
-            ev[1].record(st)
             if self.rank == 0:
+                if self.nmine:
+                    self._render_into(self.locals[slot], 0, self.nmine)
+                ev[1].record(st)
                 self._scatter(slot)
             else:
-                self._encode(slot)
+                # render + encode in one kernel (the scan and compaction after it count as the pack)
+                self._render_message(slot)
+                ev[1].record(st)
                 self.size_host[slot].copy_(self.size_dev[slot], non_blocking=True)
                 self.size_ev[slot].record(st)
             ev[2].record(st)

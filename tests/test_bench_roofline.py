@@ -158,14 +158,13 @@ def test_post_line_fracs_below_peak():
 
 def test_post_bytes_model():
     P = bench.post_plan(4096, 4096)
-    assert (P["d1"], P["d2"], P["pyramid"], P["chain"]) == (7, 8, True, True)
+    assert (P["d1"], P["d2"], P["pyramid"]) == (7, 8, True)
     px = 4 * 4096 * 4096
     bl, ch = bench.post_bytes(4096, 4096, "bloom"), bench.post_bytes(4096, 4096, "chain")
     # bloom of a frame reads it twice (pyramid, base texel) and writes it once;
-    # the chain reads the FXAA frame once for bloom (the mips start at level 3)
+    # the chain is FXAA's frame in and out plus bloom of it
     assert 3 * px < bl["total"] < 3.05 * px
-    assert ch["kernels"]["mips"] < px / 50
-    assert ch["total"] < bench.post_bytes(4096, 4096, "fxaa")["total"] + bl["total"] - 0.9 * px
+    assert ch["total"] == bench.post_bytes(4096, 4096, "fxaa")["total"] + bl["total"]
     # lod <= 0: one kernel, frame in and out
     assert bench.post_bytes(64, 16, "bloom")["kernels"] == {"bloom": 2 * 4 * 64 * 16}
 

@@ -2,27 +2,27 @@
 them (rm_post_chain): FXAA (post.frag:16-61) into postTexture, its mip chain
 (generateMipmap), bloom.frag:14-43 of it.
 
-* bit for bit the oracle's chain, oracle.bloom(oracle.fxaa(frame)), on a frame
-  of a size whose chain takes the fused path (the FXAA kernel writes mip level
-  3 of its output, BloomPlan::chain) and on sizes that do not;
+* bit for bit the oracle's chain, oracle.bloom(oracle.fxaa(frame)), on frames
+  whose mips take the exact-halving pyramid (256 x 2560, 512 x 512) and the
+  per-level resample (200 x 150);
 * bit for bit rm_fxaa followed by rm_bloom, up to the C3 frame (4096^2);
-* the plan's chain predicate (C++ bloom_plan) restated in bench.post_plan.
+* bench.post_plan's restatement of the C++ bloom_plan's mip path.
 """
 import numpy as np
 import pytest
 
 import oracle
 
-# (W, H, chain): the fused path needs W, H multiples of 2^d2 with d2 - 3 in
-# [5, 8] (d2 = floor(log2(0.05 H)) + 1) and of the FXAA tile (64 x 32)
-SIZES = [(256, 2560, True), (4096, 4096, True), (512, 512, False), (1920, 1080, False), (200, 150, False),
+# (W, H, pyramid): the exact-halving pyramid needs W, H multiples of 2^d2
+# (d2 = floor(log2(0.05 H)) + 1) and 5 to 8 levels below its start
+SIZES = [(256, 2560, True), (4096, 4096, True), (512, 512, True), (1920, 1080, False), (200, 150, False),
          (8192, 8192, True)]
 
 
-@pytest.mark.parametrize("W,H,chain", SIZES)
-def test_chain_predicate(W, H, chain):
+@pytest.mark.parametrize("W,H,pyramid", SIZES)
+def test_mip_path(W, H, pyramid):
     import bench
-    assert bench.post_plan(W, H)["chain"] == chain
+    assert bench.post_plan(W, H)["pyramid"] == pyramid
 
 
 def _frame(R, W, H, kind):

@@ -1,7 +1,7 @@
 """Post-pass driver for rocprofv3 runs: one 4096^2 scene-T RGBA8 frame, then
 `reps` passes of `fxaa`, `bloom` or `post_chain` (FXAA then bloom of its
 output, rm_post_chain) over it (tools/; not part of the product).
-Usage: post_probe.py fxaa|bloom|post_chain [W] [H] [reps]"""
+Usage: post_probe.py fxaa|bloom|post_chain|fxaa_bloom [W] [H] [reps]"""
 import os
 import sys
 
@@ -24,6 +24,9 @@ mid = torch.empty_like(frame)
 for _ in range(reps):
     if which == "post_chain":
         r.post_chain(frame, mid=mid, out=out)
+    elif which == "fxaa_bloom":  # the two passes as separate calls (rm_fxaa, then rm_bloom of its output)
+        r.fxaa(frame, out=mid)
+        r.bloom(mid, out=out)
     else:
         getattr(r, which)(frame, out=out)
 torch.cuda.synchronize()

@@ -14,7 +14,14 @@ the result; the driver's 8-GPU run measures the real gather (bench.py
 gather_ms).  Both the even split (bands of 16) and bench.py's balanced split
 (balanced_runs, sized with the same link assumption) are modelled.
 
-Usage: scale_model.py [--config C3|C5] [--ns 1,2,4,8] [--frames 24] [--link-gbs 64]
+--wire delta models the compressed wire (DeltaFrame) instead:
+every non-root rank renders straight into its message
+(rm_render_cycle_rows_wire, the encode in the render kernel's epilogue, plus
+the scan and compaction), the root renders its rows and copies them into the
+frame, then decodes the other parts' messages (one rm_wire_decode_parts
+launch, timed alone on their real messages); the link carries the messages.
+
+Usage: scale_model.py [--config C3|C5] [--ns 1,2,4,8] [--frames 24] [--link-gbs 64] [--wire rgb8|delta]
 One JSON line per (N, split)."""
 import argparse
 import json
@@ -48,6 +55,7 @@ def cumask_stream(torch):
 
 STREAM_KIND = "pool"
 KEPT = False  # --kept: frame streams bound with rm_set_stream_kept, as DistributedFrame binds them
+WIRE = "rgb8"
 
 
 def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
@@ -67,14 +75,28 @@ def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     loc = [torch.empty((n, W), dtype=torch.int32, device="cuda") for _ in streams]
     wire = [torch.empty((n, 3 * W), dtype=torch.uint8, device="cuda") for _ in streams]
+    delta = WIRE == "delta"
+    if delta:
+        import raymarching_amd as rm
+        msg = [torch.empty(rm.wire_capacity(W, n), dtype=torch.uint8, device="cuda") for _ in streams]
+        ws = [torch.empty(rm.wire_workspace_bytes(W, n), dtype=torch.uint8, device="cuda") for _ in streams]
+        size = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in streams]
+        frame = torch.empty((p.H, W), dtype=torch.int32, device="cuda") if rank == 0 else None
 
     def one(i):
         k = i % nstreams
         st = streams[k]
         with torch.cuda.stream(st):
             r.set_stream(st, kept=KEPT)
-            r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[k])
-            r.pack_rgb8(loc[k], out=wire[k])
+            if not delta:
+                r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[k])
+                r.pack_rgb8(loc[k], out=wire[k])
+            elif rank == 0:  # its rows into the frame (the decode of the others is timed apart)
+                r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[k])
+                r.scatter_part_rgba8(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], n, loc[k], frame)
+            else:
+                r.render_cycle_rows_wire(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, msg[k], ws[k],
+                                         size[k])
         r.set_stream(streams[0], kept=KEPT)
 
     t_end = time.time() + 0.3
@@ -92,7 +114,32 @@ def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
     r.set_stream(streams[0])
     ks = sorted(r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[0],
                                     stats=True)[1]["kernel_ms"] for _ in range(7))
+    if delta and rank > 0:  # this rank's message (the last frame's), for the root's decode and the link
+        torch.cuda.synchronize()
+        k = int(size[0].item())
+        MESSAGES[rank] = (msg[0][:k].clone(), n)
     return ms, ks[len(ks) // 2]
+
+
+MESSAGES = {}  # rank -> (message, rows) of the last modelled plan (--wire delta)
+
+
+def decode_ms(r, torch, plan):
+    """The root's decode of every other part's message into the frame (one launch)."""
+    W, H = plan.W, plan.H
+    frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    qs = list(range(1, plan.nshards))
+    args = (W, H, plan.cycle, [plan.offsets[q] for q in qs], [plan.part_runs[q] for q in qs],
+            [MESSAGES[q][1] for q in qs], [MESSAGES[q][0] for q in qs], frame)
+    for _ in range(10):
+        r.wire_decode_parts(*args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(30):
+        r.wire_decode_parts(*args)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 30
 
 
 def deinterleave_ms(r, torch, plan):
@@ -122,13 +169,15 @@ def main():
     ap.add_argument("--even-only", action="store_true")
     ap.add_argument("--kept", action="store_true", help="bind the frame streams as kept (no marker per leave)")
     ap.add_argument("--stream-kind", default="probed", choices=["pool", "cumask", "probed"])
+    ap.add_argument("--wire", default="rgb8", choices=["rgb8", "delta"])
     ap.add_argument("--link-gbs", type=float, default=64.0,
                     help="assumed xGMI rate of one link, one direction, as RCCL point-to-point achieves it (GB/s)")
     args = ap.parse_args()
     import torch
-    global STREAM_KIND, KEPT
+    global STREAM_KIND, KEPT, WIRE
     STREAM_KIND = args.stream_kind
     KEPT = args.kept
+    WIRE = args.wire
 
     import raymarching_amd as rm
     from bench import balanced_runs
@@ -144,10 +193,13 @@ def main():
     link_bpms = args.link_gbs * 1e6  # bytes per ms
     for N in [int(x) for x in args.ns.split(",")]:
         even = ShardPlan(W, H, args.band if N > 1 else H, N, None if N > 1 else (H,))
+        MESSAGES.clear()
         per = [per_frame_ms(r, torch, even, q, args.frames, args.streams) for q in range(N)]
-        d = deinterleave_ms(r, torch, even) if N > 1 else 0.0
+        d = (decode_ms(r, torch, even) if args.wire == "delta" else deinterleave_ms(r, torch, even)) if N > 1 else 0.0
+        wire_even = ([0] + [int(MESSAGES[q][0].numel()) for q in range(1, N)] if args.wire == "delta" and N > 1
+                     else None)
         rows = {"even": (even, per, d)}
-        if N > 1 and not args.even_only:
+        if N > 1 and not args.even_only and args.wire == "rgb8":
             ex = {"render_ms": [x[0] for x in per], "gather_ms": max(even.count(q) for q in range(1, N)) * 3 * W
                   / link_bpms, "deinterleave_ms": d}
             runs, model = balanced_runs(N, args.band, H, ex)
@@ -155,15 +207,17 @@ def main():
             perb = [per_frame_ms(r, torch, bal, q, args.frames, args.streams) for q in range(N)]
             rows["balanced"] = (bal, perb, deinterleave_ms(r, torch, bal))
         for name, (plan, pr, dms) in rows.items():
-            wire = [plan.count(q) * 3 * W for q in range(N)]
+            wire = wire_even if wire_even is not None else [plan.count(q) * 3 * W for q in range(N)]
             link = max(wire[1:], default=0) / link_bpms
             compute = [pr[0][0] + dms] + [x[0] for x in pr[1:]]
             frame = max(max(compute), link)
             print(json.dumps({
-                "config": args.config, "N": N, "split": name, "streams": args.streams, "stream_kind": args.stream_kind, "runs": list(plan.part_runs),
+                "config": args.config, "N": N, "split": name, "wire": args.wire, "streams": args.streams,
+                "stream_kind": args.stream_kind, "runs": list(plan.part_runs),
                 "per_rank_frame_ms": [round(x[0], 4) for x in pr],
                 "per_rank_kernel_ms": [round(x[1], 4) for x in pr],
-                "deinterleave_ms": round(dms, 4), "wire_bytes": wire, "link_gbs_assumed": args.link_gbs,
+                ("root_decode_ms" if args.wire == "delta" else "deinterleave_ms"): round(dms, 4), "wire_bytes": wire,
+                "link_gbs_assumed": args.link_gbs,
                 "link_ms": round(link, 4), "projected_frame_ms": round(frame, 4),
                 "bound": "link" if link >= max(compute) else ("root" if compute[0] >= max(compute[1:], default=0)
                                                               else "rank"),
