@@ -360,26 +360,18 @@ bool is_device_ptr(const void *p) {
 }
 
 // Workgroups at the head of an ordered launch that render scene T with the
-// latency-optimized folds (FrameConst.lat_tiles); RM_LAT_TILES overrides the
-// default (tuning).
-int lat_tiles() {
-    static const int n = [] {
-        const char *e = std::getenv("RM_LAT_TILES");
-        return e ? std::max(0, std::atoi(e)) : 2048;
-    }();
-    return n;
-}
+// latency-optimized folds (FrameConst.lat_tiles) ...
+constexpr int kLatTiles = 2048;
 // ... in launches short enough for their tail to show: a rank's share, a 1080p
 // frame.  The C4 share at N = 8 (32768 tiles) takes 0.077 ms per pipelined
 // frame with them and 0.098 without; a whole 4096^2 frame (262144 tiles) runs
 // 0.4 % faster without them, an N = 2 half frame (131072) the same either way
 // (profiles/r05/knob_lat_r05.log, lat_share_r05.jsonl): launches of more tiles
-// than this take none (an RM_LAT_TILES setting applies to every launch).
+// than this take none.
 constexpr int64_t kLatMaxTiles = 98304;
 int lat_tiles_for(int kernel, int W, int nrows) {
-    static const bool forced = std::getenv("RM_LAT_TILES") != nullptr;
     const rm::TileGrid g = rm::tile_grid(kernel, W, nrows);
-    return forced || (int64_t)g.x * g.y <= kLatMaxTiles ? lat_tiles() : 0;
+    return (int64_t)g.x * g.y <= kLatMaxTiles ? kLatTiles : 0;
 }
 
 // Launches per dispatch-order sort of a geometry (rm_ctx::Sched): 16 -- an
@@ -392,29 +384,18 @@ int lat_tiles_for(int kernel, int W, int nrows) {
 // Round 4 sorts on the frame's stream (21 us per sort in the frame's time):
 // 16 measured 0.3-0.7 % faster than 8 still, walking and at P1, 4 slower
 // (profiles/r04/sched_knobs_final_ab.log, sched_period_walk_p1_ab.log).
-// RM_SCHED_PERIOD overrides it (1 = re-sort after every launch).
-int sched_period() {
-    static const int n = [] {
-        const char *e = std::getenv("RM_SCHED_PERIOD");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 16;
-    }();
-    return n;
-}
+constexpr int kSchedPeriod = 16;
+int sched_period() { return kSchedPeriod; }
 
-// Dilation radius (tiles) of the sort key (rm_kernels.hip tile_key):
-// RM_SCHED_DILATE, default 2.  With a moving camera (bench.py --walk) the
-// costly regions move between the launch that measured the durations and
-// the launches that use the order: undilated, C3 walks at 0.457 ms per frame
-// against row-major's 0.440; radius 2 0.439, with the still pose unchanged
-// (0.583 ms, row-major 0.633); radius 4 0.437 walking but 0.589 still
-// (profiles/r03/sched_walk_dilate.jsonl).
-int sched_dilate() {
-    static const int n = [] {
-        const char *e = std::getenv("RM_SCHED_DILATE");
-        return e ? std::max(0, std::min(8, std::atoi(e))) : 2;
-    }();
-    return n;
-}
+// Dilation radius (tiles) of the sort key (rm_kernels.hip tile_key): 2.  With
+// a moving camera (bench.py --walk) the costly regions move between the launch
+// that measured the durations and the launches that use the order:
+// undilated, C3 walks at 0.457 ms per frame against row-major's 0.440; radius
+// 2 0.439, with the still pose unchanged (0.583 ms, row-major 0.633); radius 4
+// 0.437 walking but 0.589 still (profiles/r03/sched_walk_dilate.jsonl, DESIGN.md
+// 2.6).
+constexpr int kSchedDilate = 2;
+int sched_dilate() { return kSchedDilate; }
 
 // The frame rows one launch renders: y with (y mod cycle) - offset in [0, run)
 // (round-robin bands: run = band, cycle = band * nshards, offset = band * shard).

@@ -213,8 +213,8 @@ __device__ __forceinline__ float sponge_box(V3 p) {
 // d >= 1/s the remaining folds cannot raise d (the `if (c > d)` of
 // common.frag:671 never fires) and the result is exactly d.  Lanes that are
 // not `active` never ask for a fold.  Far from the sponge (most march and
-// shadow steps) whole waves skip the folds.  The exit test is wave-uniform
-// (RM_FOLD_UNIFORM): a wave computes fold m if any of its lanes needs it, and
+// shadow steps) whole waves skip the folds.  The exit test is wave-uniform:
+// a wave computes fold m if any of its lanes needs it, and
 // lanes past their exit point compute a fold that leaves d unchanged.  The
 // same VALU as a per-lane branch, without the two exec-mask SALU per test
 // (v_cmp to vcc + s_cbranch_vccz), and SALU issue is a co-bottleneck
@@ -225,9 +225,6 @@ __device__ __forceinline__ float sponge_box(V3 p) {
 // default) executes the fewest instructions, 1 the fewest branches and exec-mask
 // updates, which is what bounds the latency of a lone long wave (the tail of a
 // launch: render_tile's latency tiles).
-#ifndef RM_FOLD_UNIFORM
-#define RM_FOLD_UNIFORM 1
-#endif
 template <bool EXACT, int NB = 3>
 __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool active = true) {
     constexpr float SH[3] = {0.5f, 1.5f, 4.5f};                      // s/2 before s *= 3
@@ -238,11 +235,7 @@ __device__ __forceinline__ float sponge_folds(V3 p, float d, uint32_t& fl, bool 
     for (int m = 0; m < 3; m++) {
         need = active && d < INV[m];  // (d only grows: implies the earlier tests)
         if (m < NB) {
-#if RM_FOLD_UNIFORM
             if (__builtin_amdgcn_ballot_w64(need) == 0) return d;
-#else
-            if (!need) return d;
-#endif
         }
         if (need) fl += FL_FOLD;
         float rx, ry, rz;
@@ -330,18 +323,12 @@ __device__ __forceinline__ float menger_at(const LinRay& r, float t, Tally& n, b
 // in the distance; m unused) is s = x^3 / (6 k^2) in three operations and the
 // closer distance as one IEEE minimum (the same value as aCloser ? a : b for
 // non-NaN distances): 7 VALU instead of 12 without contraction.
-// RM_SMIN_EXACT_MINIMUM: the exact form's closer distance as one IEEE
-// minimum instead of compare + select (+ a hazard s_nop): C5 frame 9.89 ->
+// The exact form's closer distance is one IEEE minimum too, instead of
+// compare + select (+ a hazard s_nop): C5 frame 9.89 ->
 // 9.59 ms, frames identical (profiles/r03/scene_O_micro_ab.jsonl)
-#ifndef RM_SMIN_EXACT_MINIMUM
-#define RM_SMIN_EXACT_MINIMUM 1
-#endif
-#ifndef RM_SMIN_PROBE_FAST
-#define RM_SMIN_PROBE_FAST 1
-#endif
 template <bool EXACT>
 __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& m) {
-    if constexpr (!EXACT && RM_SMIN_PROBE_FAST) {
+    if constexpr (!EXACT) {
         const float x = fmaxf(k - fabsf(a - b), 0.0f);
         m = 0.0f;
         return fmaf(-(x * x), x * (1.0f / (6.0f * k * k)), __builtin_elementwise_minimum(a, b));
@@ -350,22 +337,15 @@ __device__ __forceinline__ float smin_cubic_d(float a, float b, float k, float& 
     float h = EXACT ? div_const(x, k, 1.0f / k) : x * (1.0f / k);
     m = h * h * h * 0.5f;
     float s = m * k * (1.0f / 3.0f);
-#if RM_SMIN_EXACT_MINIMUM  // (aCloser ? a : b) as one IEEE minimum: equal for non-NaN distances up to the sign of a zero
     return __builtin_elementwise_minimum(a, b) - s;
-#else
-    return (a < b ? a : b) - s;
-#endif
 }
 
 // FUSE_O: scene O's probe form (its sphere and cube distances, !EXACT) fuses
-// the sum of squares (RM_PROBE_FMA_O, rm_render_direct.h); every other caller
+// the sum of squares (as its probe points, rm_render_direct.h); every other caller
 // (scene S0's sphere) keeps the unfused form
-#ifndef RM_PROBE_FMA_O
-#define RM_PROBE_FMA_O 1
-#endif
 template <bool EXACT, bool FUSE_O = false>
 __device__ __forceinline__ float len3(float x, float y, float z) {
-    if constexpr (!EXACT && FUSE_O && RM_PROBE_FMA_O) return __builtin_amdgcn_sqrtf(fmaf(z, z, fmaf(y, y, x * x)));
+    if constexpr (!EXACT && FUSE_O) return __builtin_amdgcn_sqrtf(fmaf(z, z, fmaf(y, y, x * x)));
     float l2 = x * x + y * y + z * z;
     return EXACT ? sqrtf(l2) : __builtin_amdgcn_sqrtf(l2);
 }
@@ -390,12 +370,6 @@ __device__ __forceinline__ float cube(V3 p, V3 c, float r) {
 // margin over what exactness needs; rounding of the extrapolation is ~1e-5.
 // Callers use it to replace whole spans of rays and whole probe sets of a
 // shading point by the plane (PlaneSpan, rm_render_direct.h).
-#ifndef RM_O_ONE_FOLD
-#define RM_O_ONE_FOLD 0
-#endif
-#ifndef RM_O_LBS1  // C5 frame 10.22 -> 10.07 ms (profiles/r03/scene_O_micro_ab.jsonl)
-#define RM_O_LBS1 1
-#endif
 template <bool EXACT>
 __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n, float& slack) {
     n.evals++;
@@ -405,51 +379,11 @@ __device__ __forceinline__ float scene_dist_O(V3 p, V3 q, Tally& n, float& slack
     // distance, exactly also after rounding), and sminCubic lowers the min
     // by at most k/6: if even the bound of t1 is past the floor by more than
     // the blend width, t2 = sminCubic(t1, plane) is exactly the plane.
-#if RM_O_LBS1  // (one subtraction: the bounds decide branches with 0.01 of margin, never a value)
     const float lbs = fminf(fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))),
                             fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f)))) - 1.0834f;
     n.flop += FL_BOUNDS + FL_BOX + 1;
-#else
-    float lb1 = fmaxf(fabsf(p.x - 3.0f), fmaxf(fabsf(p.y - 2.0f), fabsf(p.z - 3.0f))) - 1.0f;
-    float lb2 = fmaxf(fabsf(p.x + 5.0f), fmaxf(fabsf(p.y - 4.0f), fabsf(p.z - 5.0f))) - 1.0f;
-    n.flop += FL_BOUNDS + FL_BOX + 1;
-    const float lbs = fminf(lb1, lb2) - 0.0834f;
-#endif
     const float mc = sponge_box(q);
     slack = fminf(lbs - (d3 + 0.51f), mc - (d3 + 0.34f));
-#if RM_O_ONE_FOLD
-    // The same three cases as below (the plane; the sponge folded first; the
-    // sphere/cube blend t2 first), with ONE inlined copy of the folds: in a
-    // wave whose lanes fall in different cases the three call sites below each
-    // ran the folds for their lanes.  t2 = T2() is a pure function of p, and
-    // where lbs >= d3 + 0.51 it is d3 bit for bit (h = 0 in both blends), so
-    // t2 is computed before the folds for every lane of a wave that holds a
-    // lane needing it first (one wave-uniform branch, no exec-mask change), and
-    // after them only in a wave that has not computed it and still holds a
-    // folded lane that needs it.  Every lane returns the value of the
-    // expression it returned before.
-    {
-        const bool plane = lbs >= d3 + 0.51f;
-        const float A = fminf(lbs, d3) - 0.0834f;
-        const bool folded = !plane && mc + 0.34f <= A;
-        auto T2 = [&]() {
-            const float d1 = len3<EXACT, true>(p.x - 3.0f, p.y - 2.0f, p.z - 3.0f) - 1.0f;
-            const float d2 = cube<EXACT>(p, v3(-5.0f, 4.0f, 5.0f), 1.0f);
-            return smin_cubic_d<EXACT>(smin_cubic_d<EXACT>(d1, d2, 0.5f, m), d3, 0.5f, m);
-        };
-        float t2 = d3;
-        const bool have_t2 = __builtin_amdgcn_ballot_w64(!plane & !folded) != 0;  // (wave-uniform)
-        if (have_t2) t2 = T2();
-        if (!plane & !folded) n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
-        if (!folded && mc >= t2 + 0.34f) return t2;  // plane lanes: t2 = d3, the plane test
-        const float d0 = sponge_folds<EXACT>(q, mc, n.flop);
-        if (folded && d0 + 0.34f <= A) return d0;
-        if (folded) n.flop += FL_SPHERE + FL_CUBE + 2 * FL_SMIN;
-        if (!have_t2 && __builtin_amdgcn_ballot_w64(folded) != 0) t2 = T2();
-        n.flop += FL_SMIN;
-        return smin_cubic_d<EXACT>(d0, t2, 0.33f, m);
-    }
-#endif
     // The sponge d0 >= its box term mc.  If mc - t2 exceeds the blend width
     // k = 0.33 (with a margin far above rounding), sminCubic's h is 0 and the
     // result is exactly t2: the sponge's folds are not needed.
@@ -547,24 +481,15 @@ __device__ __forceinline__ Mat mat_mirror() {  // output_shader.frag:15
     return mat_make(v3s(0.1f), v3s(0.09f), 64.0f, 0.25f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
 }
 // output_shader.frag:16-28
-// (colour only: with RM_FAST_COLOUR the blur width and the divisions by it in
-// the hardware forms; smoothstep is 150-Lipschitz here, so 1-ulp changes of its
+// (colour only: the blur width and the divisions by it in the hardware
+// forms; smoothstep is 150-Lipschitz here, so 1-ulp changes of its
 // argument move the colour by ~1e-5 at most)
-#ifndef RM_FAST_COLOUR
-#define RM_FAST_COLOUR 1
-#endif
 __device__ __forceinline__ Mat floor_mat(V3 pos) {
-#if RM_FAST_COLOUR
     const float l2 = dot(pos, pos);
     const float scale = fmaxf(10.0f, __builtin_amdgcn_exp2f(0.65f * __builtin_amdgcn_logf(l2)));  // |pos|^1.3
     const float is = __builtin_amdgcn_rcpf(scale);
     float tx = smoothstep(-0.005f, 0.005f, glsl_sin(pos.x * PI_REF) * is);
     float ty = smoothstep(-0.005f, 0.005f, glsl_sin(pos.z * PI_REF) * is);
-#else
-    float scale = fmaxf(10.0f, powf(length(pos), 1.3f));
-    float tx = smoothstep(-0.005f, 0.005f, glsl_sin(pos.x * PI_REF) / scale);
-    float ty = smoothstep(-0.005f, 0.005f, glsl_sin(pos.z * PI_REF) / scale);
-#endif
     float tile = fminf(fmaxf(tx, ty), fmaxf(1.0f - tx, 1.0f - ty));
     V3 color = mix3(v3s(0.3f), v3s(0.025f), tile);
     return mat_make(color, v3s(0.03f), 128.0f, 0.0f, 0.0f, v3s(0.0f), 1.0f, v3s(0.0f));
@@ -613,15 +538,12 @@ __device__ __forceinline__ float gpow(float x, float y) {
     if constexpr (FAST) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
     else return powf(x, y);
 }
-// RM_FAST_SHADE (scenes S0/T, FAST): the colour path's division and exp as
+// FAST (scenes S0/T): the colour path's division and exp as
 // the hardware reciprocal and exp2 (1 ulp; the colour is smooth in them):
 // arcp division had compiled to a frexp/ldexp-scaled reciprocal, 8 VALU each
-#ifndef RM_FAST_SHADE
-#define RM_FAST_SHADE 1
-#endif
 template <bool FAST>
 __device__ __forceinline__ float tonemap1(float c, float e2) {
-    float col = FAST && RM_FAST_SHADE ? (c * 2.0f) * __builtin_amdgcn_rcpf(1.0f + c) : c * 2.0f / (1.0f + c);
+    float col = FAST ? (c * 2.0f) * __builtin_amdgcn_rcpf(1.0f + c) : c * 2.0f / (1.0f + c);
     if constexpr (FAST) {  // pow(pow(x, .4545), e2) = exp2(.4545 e2 log2 x): one log2, one exp2
         col = __builtin_amdgcn_exp2f((0.4545f * e2) * __builtin_amdgcn_logf(col));
     } else {
@@ -648,13 +570,13 @@ __device__ __forceinline__ V3 post_colour(V3 c, float v) {
 template <bool FAST = false>
 __device__ __forceinline__ V3 apply_scattering(V3 color, V3 ro, V3 p) {
     float d = 1.0f - clamp01(length(p - ro) / ZFAR);
-    float e = FAST && RM_FAST_SHADE ? __builtin_amdgcn_exp2f(d * -2.8853900817779268f) : expf(-d * 2.0f);  // 2 log2(e)
+    float e = FAST ? __builtin_amdgcn_exp2f(d * -2.8853900817779268f) : expf(-d * 2.0f);  // 2 log2(e)
     return color * (1.0f - e) + v3(0.34f, 0.435f, 0.57f) * e;
 }
 // output_shader.frag:178-182
-// (the sky's fog in the colour-only fast form with RM_FAST_COLOUR, rm_render_direct.h)
+// (the sky's fog in the colour-only fast form, as every scene's colour path, rm_render_direct.h)
 __device__ __forceinline__ V3 background(V3 ro, V3 rd) {
-    return apply_scattering<RM_FAST_COLOUR != 0>(v3s(0.0f), ro, ro + rd * ZFAR);
+    return apply_scattering<true>(v3s(0.0f), ro, ro + rd * ZFAR);
 }
 
 // RGBA8 unorm of the reference's RenderTexture: clamp, round to nearest

@@ -17,14 +17,8 @@ namespace rm {
 // less than occupancy 5 does (C5 frame 12.29 -> 11.56 ms,
 // profiles/r02/scene_O_occupancy_ab.jsonl); S0/T fit 8 waves unasked; the
 // glass test scene OG would spill ~80 VGPRs and keeps its allocation.
-#ifndef RM_WAVES_PER_EU
-#define RM_WAVES_PER_EU 1
-#endif
-#ifndef RM_O_WAVES
-#define RM_O_WAVES 8
-#endif
 template <int SC>
-constexpr int kWavesPerEU = SC == SCENE_O ? RM_O_WAVES : RM_WAVES_PER_EU;
+constexpr int kWavesPerEU = SC == SCENE_O ? 8 : 1;
 template <int SC, bool COUNT, int K, typename OUT>
 __global__ __launch_bounds__(64 * Tiling<K>::WPB) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<SC>)))
 void rm_render_direct(FrameConst F, OUT* __restrict__ out, unsigned long long* __restrict__ evals) {

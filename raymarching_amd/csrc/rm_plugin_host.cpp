@@ -222,13 +222,6 @@ std::string translation_unit(const std::string& src, const std::string& file) {
 bool compile(const std::string& src, const std::string& file, Code& code, std::string& log) {
     const std::string tu = translation_unit(src, file);
     log.clear();
-    if (const char* dump = std::getenv("RM_PLUGIN_DUMP_TU")) {  // (analysis: the translation unit hiprtc compiles)
-        FILE* f = std::fopen(dump, "w");
-        if (f) {
-            std::fwrite(tu.data(), 1, tu.size(), f);
-            std::fclose(f);
-        }
-    }
     {
         std::lock_guard<std::mutex> g(g_mu);
         auto it = g_cache.find(tu);
@@ -244,31 +237,12 @@ bool compile(const std::string& src, const std::string& file, Code& code, std::s
         log = std::string("hiprtcCreateProgram: ") + hiprtcGetErrorString(r);
         return false;
     }
-    // the flags of scene O's translation unit (raymarching_amd/Makefile), and
-    // the render kernel's occupancy (RM_PLUGIN_WAVES_PER_EU overrides it)
-    const char* env_w = std::getenv("RM_PLUGIN_WAVES_PER_EU");
-    const std::string waves = std::string("-DRM_PLUGIN_WAVES_PER_EU=") +
-                              (env_w && std::atoi(env_w) > 0 ? std::to_string(std::atoi(env_w)) : std::string("1"));
-    // (no SLP vectorization, as librm's own device code: raymarching_amd/Makefile DEVFLAGS)
+    // the flags of scene O's translation unit (raymarching_amd/Makefile), no
+    // SLP vectorization (as librm's own device code: DEVFLAGS)
     const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                           "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", "-Wno-unused-function",
-                          "-Wno-unused-variable", waves.c_str()};
-    // RM_PLUGIN_EXTRA_FLAGS (analysis only): options appended after these
-    std::vector<std::string> extra;
-    if (const char* e = std::getenv("RM_PLUGIN_EXTRA_FLAGS")) {
-        std::string w;
-        for (const char* c = e;; c++) {
-            if (*c == ' ' || *c == 0) {
-                if (!w.empty()) extra.push_back(w);
-                w.clear();
-                if (*c == 0) break;
-            } else {
-                w += *c;
-            }
-        }
-    }
+                          "-Wno-unused-variable"};
     std::vector<const char*> all(opts, opts + sizeof(opts) / sizeof(opts[0]));
-    for (const std::string& x : extra) all.push_back(x.c_str());
     r = hiprtcCompileProgram(prog, (int)all.size(), all.data());
     size_t ls = 0;
     if (hiprtcGetProgramLogSize(prog, &ls) == HIPRTC_SUCCESS && ls > 1) {

@@ -23,11 +23,6 @@ struct rm::PluginScene<rm::SCENE_PLUGIN> {
 // ray-step tallies and step maps).  One kernel serving both paid the
 // instrumented pipeline's registers in every timed launch (occupancy 5).  The
 // output format is a run-time argument.
-// Minimum waves per SIMD for the register allocator (rm_plugin_host.cpp sets
-// it, default 1 = unconstrained).
-#ifndef RM_PLUGIN_WAVES_PER_EU
-#define RM_PLUGIN_WAVES_PER_EU 1
-#endif
 namespace rm {
 template <bool COUNT>
 __device__ __forceinline__ void plugin_render_tile(const FrameConst& F, void* out, int rgba8,
@@ -72,7 +67,7 @@ __device__ __forceinline__ void plugin_render_tile(const FrameConst& F, void* ou
     }
 }
 }  // namespace rm
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_PLUGIN_WAVES_PER_EU))) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
+extern "C" __global__ __launch_bounds__(64) void rm_plugin_render(rm::FrameConst F, void* out, int rgba8,
                                                                   unsigned long long* evals) {
     rm::plugin_render_tile<false>(F, out, rgba8, evals);
 }

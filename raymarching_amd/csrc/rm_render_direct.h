@@ -34,14 +34,14 @@ __device__ __forceinline__ float mpow(float x, float y) {
     else return powf(x, y);
 }
 // Colour-only arithmetic (Phong's normalizations and pow, the shadow factor's
-// pow, the SSS term's pow, fog, tonemap, vignette): RM_FAST_COLOUR gives scenes
-// O/OG and plugins the hardware exp2/log2/rsq/rcp forms there too (1-2 ulp).
+// pow, the SSS term's pow, fog, tonemap, vignette): scenes O/OG and plugins
+// use the hardware exp2/log2/rsq/rcp forms there too (1-2 ulp).
 // Nothing that positions a ray or feeds the thickness hash changes (marches,
 // normals, the light direction and distance, the floor pattern keep their
 // exact forms), so ray-step counts are untouched and pixels move by ~1e-6.
 template <int SC>
 struct FastColour {
-    static constexpr bool value = FastMath<SC>::value || RM_FAST_COLOUR;
+    static constexpr bool value = true;  // (every scene: FastMath<SC> or the colour-only forms)
 };
 template <int SC>
 __device__ __forceinline__ float cpow(float x, float y) {
@@ -76,11 +76,6 @@ __device__ __forceinline__ V3 mnormalize(V3 a) {
 // plane-only when the slack there is >= 2.05.
 template <int SC>
 constexpr bool kPlaneSpans = SC == SCENE_O || SC == SCENE_OG;
-// RM_O_SPANS=0 (analysis only: the structural share of the plugin gap, DESIGN.md
-// 2.4) keeps scene O's code shape but never takes a plane span or plane probe set
-#ifndef RM_O_SPANS
-#define RM_O_SPANS 1
-#endif
 __device__ __forceinline__ float plane_rate(V3 d) {  // (v_rcp: 1 ulp is far inside the margin)
     return __builtin_amdgcn_rcpf(1.01f + fabsf(d.y));
 }
@@ -90,7 +85,7 @@ __device__ __forceinline__ bool plane_probes(const FrameConst& F, V3 p) {
         Tally scratch;  // (not a ray-step of the reference)
         float slack;
         (void)scene_dist_O<false>(p, sponge_space<false>(F, p), scratch, slack);
-        return RM_O_SPANS && slack >= 2.05f;
+        return slack >= 2.05f;
     } else {
         (void)F; (void)p;
         return false;
@@ -127,11 +122,6 @@ __device__ __forceinline__ V3 normal_fast(const FrameConst& F, V3 p, Tally& cnt,
 // on step exhaustion) and the point whose SdResult is returned.  One exit
 // test per step; at a hit depth is left as it was, so the hit flag and depth
 // give the three outcomes after the loop.
-// RM_O_SPAN_UNIFORM: the floor-plane span test of scene O's march and shadow
-// steps as a wave-uniform branch (see cast_ray_d)
-#ifndef RM_O_SPAN_UNIFORM
-#define RM_O_SPAN_UNIFORM 0
-#endif
 template <int SC, bool INSIDE>
 __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V3& last_q, Tally& cnt) {
     float depth = ZNEAR;
@@ -142,14 +132,7 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
         const float ia = plane_rate(rd);
         float t_plane = 0.0f, last = 0.0f;
         for (int i = 0; i < F.max_steps; i++) {
-#if RM_O_SPAN_UNIFORM
-            // (wave-uniform: a wave with a lane past its span evaluates sceneSDF on every
-            // lane; inside a span that is the plane's value bit for bit, so the lanes'
-            // results are the same, with no exec-mask split per step)
-            if (__builtin_amdgcn_ballot_w64(!(depth < t_plane)) == 0) {
-#else
             if (depth < t_plane) {
-#endif
                 res = ro.y + rd.y * depth;
                 cnt.evals++;
                 cnt.flop += 2;
@@ -158,7 +141,7 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
                 float slack;
                 cnt.flop += FL_TRANSFORM;
                 res = scene_dist_O<true>(q, sponge_space<true>(F, q), cnt, slack);
-                t_plane = RM_O_SPANS ? depth + slack * ia : 0.0f;
+                t_plane = depth + slack * ia;
             }
             last = depth;
             if (INSIDE) {
@@ -195,9 +178,6 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
 // into a "continue" block of its own, which costs 4 SALU and 2 branches per
 // step (C4 share 0.131 -> 0.119 ms, C2 P1 0.204 -> 0.188, scene O 4096^2
 // 2.97 -> 2.92; profiles/r02/shadow_p_pin_ab.jsonl).
-#ifndef RM_SHADOW_P_PIN
-#define RM_SHADOW_P_PIN 1
-#endif
 // Scene O's settle rule (soft_shadow2_T_loop states it for
 // the sponge alone).  sceneSDF >= min(d0 - 0.33/6, d3 - 0.83/6, d1 - 1.33/6,
 // d2 - 1.33/6) (each sminCubic lowers a min by at most k/6; output_shader.frag:
@@ -213,9 +193,6 @@ __device__ __forceinline__ float cast_ray_d(const FrameConst& F, V3 ro, V3 rd, V
 // changes res.  res^2 = 16 num / den (squared, as the loop keeps it).
 // oracle settle_test_O restates the rule and checks it on every step of the
 // reference's marches.
-#ifndef RM_SETTLE_O_MIN  // (C5 frame 9.59 -> 9.56 ms, profiles/r03/scene_O_micro_ab.jsonl)
-#define RM_SETTLE_O_MIN 1
-#endif
 __device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& s, float t, float maxt, float num,
                                                  float den) {
     const float L = maxt - t;
@@ -239,28 +216,16 @@ __device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& 
     const float g0 = fminf(fminf(a0, a1), fminf(a2, a3));
     const float g1 = fminf(fminf(fmaf(s0, L, a0), fmaf(s1, L, a1)), fminf(fmaf(s2, L, a2), fmaf(w.d.y, L, a3)));
     constexpr float K = (2.9f / 1.01f) * (2.9f / 1.01f) / 16.0f;
-#if RM_SETTLE_O_MIN  // the four tests as one: IEEE minimum (NaN fails) of their margins >= 0
     const float m = __builtin_elementwise_minimum(
         __builtin_elementwise_minimum(__builtin_elementwise_minimum(g0, g1) - 0.1f, K * g0 * g0 * den - num * t * t),
         K * g1 * g1 * den - num * maxt * maxt);
     return m >= 0.0f;
-#else
-    return (g0 >= 0.1f) & (g1 >= 0.1f) & (K * g0 * g0 * den >= num * t * t) & (K * g1 * g1 * den >= num * maxt * maxt);
-#endif
 }
 
-#ifndef RM_SETTLE_O
-#define RM_SETTLE_O 1
-#endif
-// RM_O_SHADOW_EXIT2: a settled lane leaves at the test, and the uniform step
-// cap is a branch of its own: the exit test no longer materializes four
-// booleans per step (C5 frame 10.22 -> 10.03 ms; profiles/r03/scene_O_micro_ab.jsonl)
-#ifndef RM_O_SHADOW_EXIT2
-#define RM_O_SHADOW_EXIT2 1
-#endif
-#ifndef RM_SETTLE_O_EVERY
-#define RM_SETTLE_O_EVERY 8  // steps between settle tests (a power of 2)
-#endif
+// A settled lane leaves at the test, and the uniform step cap is a branch of
+// its own: the exit test does not materialize four booleans per step (C5
+// frame 10.22 -> 10.03 ms; profiles/r03/scene_O_micro_ab.jsonl)
+constexpr int kSettleOEvery = 8;  // steps between settle tests (a power of 2)
 
 // common.frag:810-831, k = 4, for scenes O/OG: the probes step along the
 // world ray and its sponge-space image, and the candidate is kept squared as
@@ -268,12 +233,12 @@ __device__ __forceinline__ bool shadow_settled_O(const LinRay& w, const LinRay& 
 // SM as soft_shadow2_T_loop (0 none, 1 timed kernels: settle exit, 2
 // instrumented kernels: every step taken, those after the settle point counted
 // in cnt.skipped); O/OG only.  The settle test (~45 VALU) runs on every
-// RM_SETTLE_O_EVERY-th step: C5 frame 11.25 -> 10.51 ms with 8, 10.79 with 4
+// kSettleOEvery-th step: C5 frame 11.25 -> 10.51 ms with 8, 10.79 with 4
 // (profiles/r03/scene_O_settle_ab.jsonl).
 template <int SC, int SM = 0, bool CAP = true>
 __device__ __forceinline__ float soft_shadow2_loop(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
                                                    Tally& cnt) {
-    constexpr bool kSettle = kPlaneSpans<SC> && SM != 0 && RM_SETTLE_O;
+    constexpr bool kSettle = kPlaneSpans<SC> && SM != 0;
     const LinRay w{ro, rd}, s = sponge_ray(F, ro, rd);
     float num = 1.0f / 16.0f, den = 1.0f, P = 0.0f, h = 1.0f;  // res = 1, k = 4
     float t = mint;
@@ -284,11 +249,7 @@ __device__ __forceinline__ float soft_shadow2_loop(const FrameConst& F, V3 ro, V
         if constexpr (SM == 2) cnt.skipped += was_settled ? 1u : 0u;
         if constexpr (SC == SCENE_PLUGIN) {
             h = dist_probe<SC>(F, at(w, t), cnt);
-#if RM_O_SPAN_UNIFORM
-        } else if (__builtin_amdgcn_ballot_w64(!(t < t_plane)) == 0) {  // (as cast_ray_d)
-#else
         } else if (t < t_plane) {
-#endif
             h = fmaf(w.d.y, t, w.o.y);  // at(w, t).y
             cnt.evals++;
             cnt.flop += 2;
@@ -296,7 +257,7 @@ __device__ __forceinline__ float soft_shadow2_loop(const FrameConst& F, V3 ro, V
             float slack;
             cnt.flop += FL_LINRAY;
             h = scene_dist_O<false>(at(w, t), at(s, t), cnt, slack);
-            t_plane = RM_O_SPANS ? t + slack * ia : 0.0f;
+            t_plane = t + slack * ia;
         }
         float h2 = h * h;
         float Q = it == 1 ? 1.0f : fmaf(P, P, -h2);
@@ -306,48 +267,35 @@ __device__ __forceinline__ float soft_shadow2_loop(const FrameConst& F, V3 ro, V
         num = upd ? cn : num;
         den = upd ? cd : den;
         bool settled = false;
-        if constexpr (kSettle) {  // every RM_SETTLE_O_EVERY-th step (h >= 0.1 is implied by the rule; h >= ph: moving away)
-            if ((it & (RM_SETTLE_O_EVERY - 1)) == 0 && __builtin_amdgcn_ballot_w64((h >= 0.1f) & (h + h >= P)) != 0)
+        if constexpr (kSettle) {  // every kSettleOEvery-th step (h >= 0.1 is implied by the rule; h >= ph: moving away)
+            if ((it & (kSettleOEvery - 1)) == 0 && __builtin_amdgcn_ballot_w64((h >= 0.1f) & (h + h >= P)) != 0)
                 settled = (h >= 0.1f) & shadow_settled_O(w, s, t, maxt, num, den);
-#if RM_O_SHADOW_EXIT2
             // (a settled lane leaves here: its result needs neither P nor t)
             if constexpr (SM == 1) {
                 if (settled) break;
             }
-#endif
         }
         P = h + h;
-#if RM_SHADOW_P_PIN
         asm volatile("" : "+v"(P));  // keep P's add in the step (not in a continue block of its own)
-#endif
         t += h * 0.1f + 0.001f;  // the reference's roundings: the step count is part of parity
         if constexpr (SM == 2) {
             was_settled |= settled;
             settled = false;
         }
-#if RM_O_SHADOW_EXIT2
         if ((h < 0.001f) | !(t < maxt)) break;
         if (CAP && it >= F.shadow_max_steps) break;  // (wave-uniform)
-#else
-        if ((h < 0.001f) | !(t < maxt) | settled | (CAP && it >= F.shadow_max_steps)) break;
-#endif
     }
     return h < 0.001f ? 0.0f : sqrtf(16.0f * num / den);
 }
-// RM_O_SHADOW_UNCAPPED: the reference's uncapped march (the default) as a loop
-// copy without the step-cap test, as scene T's (soft_shadow2_T).  Round 3
+// The reference's uncapped march (the default) runs as a loop copy without
+// the step-cap test, as scene T's (soft_shadow2_T).  Round 3
 // measured no gain while the kernel spilled; without spills: C5 frame
 // 8.524 -> 8.510 ms, C5 share 1.082 -> 1.077, O 4096^2 2.219 -> 2.212, frames
 // identical (profiles/r05/ab_O_uncapped.jsonl)
-#ifndef RM_O_SHADOW_UNCAPPED
-#define RM_O_SHADOW_UNCAPPED 1
-#endif
 template <int SC, int SM = 0>
 __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd, float mint, float maxt,
                                               Tally& cnt) {
-#if RM_O_SHADOW_UNCAPPED
     if (F.shadow_max_steps == __INT_MAX__) return soft_shadow2_loop<SC, SM, false>(F, ro, rd, mint, maxt, cnt);
-#endif
     return soft_shadow2_loop<SC, SM, true>(F, ro, rd, mint, maxt, cnt);
 }
 
@@ -384,21 +332,11 @@ __device__ __forceinline__ float soft_shadow2(const FrameConst& F, V3 ro, V3 rd,
 // SM: 0 no settle test, 1 leave the march when settled (timed kernels), 2 run
 // the test and count the steps after it in cnt.skipped (instrumented kernels:
 // every reference step is still taken and counted)
-// RM_T_SHADOW_EXIT2: as RM_O_SHADOW_EXIT2 (C3 0.575 -> 0.568 ms, C2 P1
-// 0.192 -> 0.181)
-#ifndef RM_T_SHADOW_EXIT2
-#define RM_T_SHADOW_EXIT2 1
-#endif
-#ifndef RM_SETTLE_T_EVERY
-#define RM_SETTLE_T_EVERY 1  // steps between settle tests (a power of 2)
-#endif
-// RM_T_BALLOT_SPLIT: the settle gate as the AND of the two compares' own
-// masks (s_and_b64) instead of a ballot of their combined i1, which the
+// A settled lane leaves at the test, as in scene O's loop (C3 0.575 -> 0.568
+// ms, C2 P1 0.192 -> 0.181); the test runs on every step.
+// The settle gate is the AND of the two compares' own masks (s_and_b64) instead of a ballot of their combined i1, which the
 // backend materialized as a 0/1 VGPR and a v_cmp_ne per step: 2 VALU fewer per
 // shadow step, C3 0.4603-0.4626 -> 0.4527-0.4549 ms (profiles/r05/ab_settle_T.log)
-#ifndef RM_T_BALLOT_SPLIT
-#define RM_T_BALLOT_SPLIT 1
-#endif
 template <bool CAP, int NB, int SM = 0>
 __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                      Tally& cnt) {
@@ -423,12 +361,8 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
         den = upd ? cd : den;
         bool settled = false;
         if constexpr (SM != 0) {
-#if RM_T_BALLOT_SPLIT  // the two compares' own masks ANDed on the SALU (no 0/1 VGPR and v_cmp_ne per step)
             const bool any = (__builtin_amdgcn_ballot_w64(box >= 0.1f) & __builtin_amdgcn_ballot_w64(h + h >= P)) != 0;
-#else
-            const bool any = __builtin_amdgcn_ballot_w64((box >= 0.1f) & (h + h >= P)) != 0;
-#endif
-            if ((it & (RM_SETTLE_T_EVERY - 1)) == 0 && any) {
+            if (any) {
                 const float ax = fabsf(q.x), ay = fabsf(q.y), m = box + 1.0f;
                 const float sx = q.x < 0.0f ? -s.d.x : s.d.x, sy = q.y < 0.0f ? -s.d.y : s.d.y;
                 const float sz = q.z < 0.0f ? -s.d.z : s.d.z;
@@ -439,47 +373,30 @@ __device__ __forceinline__ float soft_shadow2_T_loop(const FrameConst& F, const 
                           (K * be * be * den >= num * maxt * maxt);
             }
         }
-#if RM_T_SHADOW_EXIT2
         if constexpr (SM == 1) {
             if (settled) break;  // (the result needs neither P nor t)
         }
-#endif
         P = h + h;
-#if RM_SHADOW_P_PIN
         asm volatile("" : "+v"(P));  // keep P's add in the step (not in a continue block of its own)
-#endif
         t = fmaf(h, 0.1f, t + 0.001f);
         if constexpr (SM == 2) {
             was_settled |= settled;
             settled = false;
         }
-#if RM_T_SHADOW_EXIT2
         if ((h < 0.001f) | !(t < maxt)) break;
         if (CAP && it >= F.shadow_max_steps) break;
-#else
-        if ((h < 0.001f) | !(t < maxt) | settled | (CAP && it >= F.shadow_max_steps)) break;
-#endif
     }
     return h < 0.001f ? 0.0f : __builtin_amdgcn_sqrtf(16.0f * num * __builtin_amdgcn_rcpf(den));
 }
-#ifndef RM_SHADOW_UNCAPPED_LOOP
-#define RM_SHADOW_UNCAPPED_LOOP 1
-#endif
 // The uncapped loop (the reference's, and the default) carries no step
 // counter: a uniform counter test merged into the lanes' exit mask costs 5
 // SALU per step, and SALU issue is a co-bottleneck of the kernel.
-// (Scene O's soft_shadow2 has the same split since round 5: RM_O_SHADOW_UNCAPPED.)
-#ifndef RM_SHADOW_SETTLE
-#define RM_SHADOW_SETTLE 1
-#endif
+// (Scene O's soft_shadow2 has the same split since round 5.)
 template <int NB = 3, int SETTLE = 0>
 __device__ __forceinline__ float soft_shadow2_T(const FrameConst& F, const LinRay& s, float mint, float maxt,
                                                 Tally& cnt) {
-    constexpr int ST = RM_SHADOW_SETTLE ? SETTLE : 0;
-#if RM_SHADOW_UNCAPPED_LOOP
-    if (F.shadow_max_steps == __INT_MAX__) return soft_shadow2_T_loop<false, NB, ST>(F, s, mint, maxt, cnt);
-#endif
-    return soft_shadow2_T_loop<true, NB, ST>(F, s, mint, maxt, cnt);
+    if (F.shadow_max_steps == __INT_MAX__) return soft_shadow2_T_loop<false, NB, SETTLE>(F, s, mint, maxt, cnt);
+    return soft_shadow2_T_loop<true, NB, SETTLE>(F, s, mint, maxt, cnt);
 }
 
 // castRay (common.frag:931-954) for scene T in sponge space; returns the
@@ -505,42 +422,30 @@ __device__ __forceinline__ float cast_ray_T(const FrameConst& F, const LinRay& s
     }
     return depth >= ZFAR ? ZFAR : depth;
 }
-#ifndef RM_REFLECT_STOP
-#define RM_REFLECT_STOP 1
-#endif
 
 // common.frag:850-866.  Scene O rolls the probe loop: the unrolled loop's
 // interleaved probes spilled 18 VGPRs of the 8-wave kernel to scratch, rolled
 // 4 (same frames, C5 frame 9.46 -> 9.43 ms; scene T's rolled loop measured
 // 3 % slower, profiles/r03/rolled_probes_ab.jsonl)
-#ifndef RM_AO_ROLLED_O
-#define RM_AO_ROLLED_O 1
-#endif
-// RM_PROBE_FMA_O: scenes O/OG form the probe points of AO and thickness, and
+// Scenes O/OG form the probe points of AO and thickness, and
 // the sphere / cube lengths of the probe-form distance, with fused
 // multiply-adds (these results are smooth in their roundings; the exact march
 // and normal paths, and the thickness hash of the normal, keep the GLSL's)
-#ifndef RM_PROBE_FMA_O
-#define RM_PROBE_FMA_O 1
-#endif
 template <int SC>
-constexpr bool kProbeFma = kPlaneSpans<SC> && RM_PROBE_FMA_O;
+constexpr bool kProbeFma = kPlaneSpans<SC>;
 __device__ __forceinline__ V3 fma3(V3 a, float s, V3 b) {  // a s + b, one rounding per component
     return v3(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z));
 }
 __device__ __forceinline__ float dot_fma(V3 a, V3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 
-// RM_AO_LINRAY_T: scene T's four AO probes step along the normal's
+// Scene T's four AO probes step along the normal's
 // sponge-space image (q0 + (R n) 0.2 (i + 1), one FMA per axis) instead of
 // transforming each probe point (the AO factor is smooth in the roundings;
 // step counts do not depend on it)
-#ifndef RM_AO_LINRAY_T
-#define RM_AO_LINRAY_T 1
-#endif
 template <int SC, int NB = 3>
 __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tally& cnt, bool plane = false) {
     float sum = 0.0f;
-    if constexpr (SC == SCENE_T && RM_AO_LINRAY_T) {
+    if constexpr (SC == SCENE_T) {
         const LinRay r = sponge_ray(F, pos, n);
 #pragma unroll
         for (int i = 0; i < 4; i++) sum += (1.0f / (float)(1 << i)) * menger_at<NB>(r, (float)(i + 1) * 0.2f, cnt);
@@ -553,7 +458,7 @@ __device__ __forceinline__ float ao_real(const FrameConst& F, V3 pos, V3 n, Tall
         V3 p = kProbeFma<SC> ? fma3(n, (float)(i + 1) * 0.2f, pos) : pos + (n * (float)(i + 1)) * 0.2f;
         sum += (1.0f / (float)(1 << i)) * dist_at<SC, false, NB>(F, p, cnt, plane);
     };
-    if constexpr (kPlaneSpans<SC> && RM_AO_ROLLED_O) {
+    if constexpr (kPlaneSpans<SC>) {
 #pragma unroll 1
         for (int i = 0; i < 4; i++) probe(i);
     } else {
@@ -589,18 +494,15 @@ __device__ __forceinline__ V3 phong(V3 k_d, V3 k_s, float alpha, V3 L, V3 p, V3 
 // cnt.skipped, SM 0 takes it.  dotLN is phong's own dot(L, N): the same
 // value, so the same decision.  Scene T at P0: 54 % of the shadow-march steps
 // (oracle shadow_settle back_steps), scene O 0-6 % (its floor faces the light).
-#ifndef RM_BACKFACE_SKIP
-#define RM_BACKFACE_SKIP 1
-#endif
 template <int SM, typename March>
 __device__ __forceinline__ float shadow_if_lit(float dotLN, Tally& cnt, March march) {
     const bool lit = !(dotLN < 0.0f);
-    if constexpr (SM == 1 && RM_BACKFACE_SKIP) {
+    if constexpr (SM == 1) {
         return lit ? march() : 1.0f;
     } else {
         const uint32_t e0 = cnt.evals, s0 = cnt.skipped;
         const float sha = march();
-        if constexpr (SM == 2 && RM_BACKFACE_SKIP) {
+        if constexpr (SM == 2) {
             if (!lit) cnt.skipped = s0 + (cnt.evals - e0);
         }
         (void)e0; (void)s0; (void)lit;
@@ -636,9 +538,6 @@ __device__ __forceinline__ float thickness(const FrameConst& F, V3 pos, V3 norm,
     }
     float th = 0.0f;
     V3 nn = -norm;
-#ifdef RM_THICK_UNROLL
-#pragma unroll RM_THICK_UNROLL
-#endif
     for (int i = 0; i < 32; i++) {
         float fi = (float)i;
         float sl = F.hash11[i];
@@ -669,18 +568,10 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, 
     V3 Ld = lightPos - p;
     V3 lightDir = normalize(Ld);
     float occ = ao_real<SC>(F, p, n, cnt, plane);
-#ifdef RM_ABLATE_SHADOW
-    float sha = 1.0f;
-#else
     float sha = shadow_if_lit<SETTLE>(dot(lightDir, phongN), cnt, [&] {
         return soft_shadow2<SC, SETTLE>(F, p, lightDir, 0.01f, length(Ld), cnt);
     });
-#endif
-#ifdef RM_ABLATE_SSS
-    float th = 0.5f;
-#else
     float th = thickness<SC>(F, p, n, cnt, plane);
-#endif
     mat = scene_mat<SC>(F, mq);
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, cnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
@@ -697,7 +588,7 @@ __device__ __forceinline__ V3 light_O(const FrameConst& F, V3 mq, V3 ro, V3 rd, 
 
 // output_shader.frag:218-230
 __device__ __forceinline__ float fresnel(float n2, V3 normal, V3 incident, float reflectivity) {
-    float r0 = RM_FAST_COLOUR ? (1.0f - n2) * __builtin_amdgcn_rcpf(1.0f + n2) : (1.0f - n2) / (1.0f + n2);
+    float r0 = (1.0f - n2) * __builtin_amdgcn_rcpf(1.0f + n2);  // (colour only: the hardware reciprocal)
     r0 *= r0;
     float x = 1.0f + dot(normal, incident);
     float r = r0 + (1.0f - r0) * x * x * x * x * x;
@@ -790,40 +681,19 @@ __device__ __forceinline__ V3 render_T(const FrameConst& F, V3 ro, V3 rd, Tally&
     constexpr int SC = SCENE_T;
     V3 p = ro + rd * cast_ray_T<NB>(F, sponge_ray(F, ro, rd), cnt);
     V3 n = normal_fast<SC, NB>(F, p, cnt);
-#ifdef RM_DOUBLE_NORMAL  // (analysis: the normal's cost, evaluated twice, same frame)
-    {
-        Tally c2;
-        const V3 n2 = normal_fast<SC, NB>(F, p + v3s(1e-7f), c2);
-        n = n + n2 * 0.0f;
-    }
-#endif
     // getColorReflect (common.frag:991-1002); its dead nr normal is skipped
     V3 rdir = reflect(rd, n);
     V3 ror = p + rdir * 0.01f;
-#ifdef RM_ABLATE_REFLECT
-    V3 pr = ror;
-#else
-    V3 pr = ror + rdir * cast_ray_T<NB, RM_REFLECT_STOP ? RSTOP : 0>(F, sponge_ray(F, ror, rdir), cnt);
-#endif
+    V3 pr = ror + rdir * cast_ray_T<NB, RSTOP>(F, sponge_ray(F, ror, rdir), cnt);
     float c = clamp01(length(pr - p) * (1.0f / 3.0f));
     const V3 lightPos = v3(20.0f, 50.0f, 0.0f);
     V3 Ld = lightPos - p;
     float ld2 = dot(Ld, Ld);
     V3 lightDir = Ld * __builtin_amdgcn_rsqf(ld2);
     float occ = ao_real<SC, NB>(F, p, n, cnt);
-#ifdef RM_DOUBLE_AO  // (analysis: the AO's cost, evaluated twice, same frame)
-    {
-        Tally c2;
-        occ = occ + ao_real<SC, NB>(F, p + v3s(1e-7f), n, c2) * 0.0f;
-    }
-#endif
-#ifdef RM_ABLATE_SHADOW
-    float sha = 1.0f;
-#else
     float sha = shadow_if_lit<RSTOP>(dot(lightDir, n), cnt, [&] {
         return soft_shadow2_T<NB, SETTLE>(F, sponge_ray(F, p, lightDir), 0.01f, __builtin_amdgcn_sqrtf(ld2), cnt);
     });
-#endif
     float sky = clamp01(0.5f + 0.5f * n.y);
     float ind = clamp01(dot(n, mnormalize<SC>(lightDir * v3(-1.0f, 0.0f, -1.0f))));
     float fre = clamp01(1.0f + dot(n, rd));
@@ -967,9 +837,6 @@ template <> struct Tiling<KERNEL_PERSIST> : Tiling<KERNEL_TILE8> {};
 // evals[0..2] (ray-steps, FLOP, ray-steps the timed kernels skip).
 // (bx, by): the tile's position in dispatch order on a gx-wide tile grid
 // (blockIdx for the hardware-dispatched kernels).
-#ifndef RM_LAT_SETTLE
-#define RM_LAT_SETTLE 0
-#endif
 template <int SC, bool COUNT, int K, typename OUT>
 __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restrict__ out,
                                                unsigned long long* __restrict__ evals, int bx, int by, int gx) {
@@ -1006,7 +873,7 @@ __device__ __forceinline__ void render_tile_at(const FrameConst& F, OUT* __restr
             // (no settle exit in the latency tiles: their long grazing shadow marches
             // settle late or never, and the test lengthens the lone waves that end
             // the launch: C4 share +16 %, C2 P1 +12 % with it)
-            if (lat) c = render_pixel<SC, 1, RM_LAT_SETTLE ? (COUNT ? 2 : 1) : 0, COUNT ? 2 : 1>(F, ro, rd, cnt);
+            if (lat) c = render_pixel<SC, 1, 0, COUNT ? 2 : 1>(F, ro, rd, cnt);
             else c = render_pixel<SC, 3, COUNT ? 2 : 1, COUNT ? 2 : 1>(F, ro, rd, cnt);
         } else {
             (void)lat;

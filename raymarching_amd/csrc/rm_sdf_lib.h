@@ -44,22 +44,11 @@ namespace glsl {
 #define RM_LIB_PROBE 0
 #include "rm_sdf_lib_body.h"
 #undef RM_LIB_PROBE
-// RM_PROBE_REASSOC (analysis): the probe instance (and a plugin scene's probe
-// instance, rm_plugin_host.cpp) also with reassociation
-#ifndef RM_PROBE_REASSOC
-#define RM_PROBE_REASSOC 0
-#endif
 namespace probe {
 #pragma clang fp contract(fast)
-#if RM_PROBE_REASSOC
-#pragma clang fp reassociate(on)
-#endif
 #define RM_LIB_PROBE 1
 #include "rm_sdf_lib_body.h"
 #undef RM_LIB_PROBE
-#if RM_PROBE_REASSOC
-#pragma clang fp reassociate(off)
-#endif
 #pragma clang fp contract(off)
 }  // namespace probe
 }  // namespace glsl
