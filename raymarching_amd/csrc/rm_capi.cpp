@@ -839,10 +839,13 @@ rm_status rm_destroy(rm_ctx *ctx) {
     // nothing this context enqueued still runs: its own events (the streams
     // it left may be the caller's and gone by now); other work on the device
     // is not waited for
-    // The bound stream must still exist (rm.h: HIP does not validate stream
-    // handles, so a record on a destroyed one is undefined, not an error).  A
-    // record that does report an error leaves the context's work un-waitable
-    // by event, so the whole device is waited for.
+    // The bound stream must still exist: HIP does not validate stream handles,
+    // and a record on a destroyed one faults inside the runtime (a test saw
+    // SIGSEGV) instead of returning an error, so the lifetime rule of rm.h
+    // (rm_set_stream) is the only protection there.  The fallback below covers
+    // only a record that does return an error (e.g. a device fault): the
+    // context's work can then not be waited for by event, and the whole device
+    // is.
     bool lost = record_sched_last(ctx) != hipSuccess;
     if (ctx->done && ctx->dirty) {
         if (hipEventRecord(ctx->done, ctx->stream) == hipSuccess) (void)hipEventSynchronize(ctx->done);

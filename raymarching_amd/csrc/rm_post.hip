@@ -350,10 +350,7 @@ __global__ __launch_bounds__(256) void rm_bloom_poly_kernel(BloomAxes axes, Bloo
     dst[2] = make_float4((float)(P[8] * lam), (float)(P[9] * lam), (float)(P[10] * lam), (float)(P[11] * lam));
 }
 
-#ifndef RM_BLOOM_ROWS
-#define RM_BLOOM_ROWS 16
-#endif
-constexpr int kBloomRows = RM_BLOOM_ROWS;
+constexpr int kBloomRows = 16;  // (strip A/B, profiles/r06/bloom_strip_ab.log)
 template <typename T>
 __device__ __forceinline__ T sload_entry(const T* base, int i) {  // a wave-uniform 8-byte entry via the scalar cache
     static_assert(sizeof(T) == 8, "8-byte entries");
@@ -404,11 +401,9 @@ __device__ __forceinline__ RGB base_bilinear(const uint32_t* r0, const uint32_t*
 
 // One lane per column of a kBloomRows strip, the rows in batches of
 // kBloomBatch whose texel loads are issued together (the loads in flight per
-// wave, not the arithmetic, bound a lone strip).
-#ifndef RM_BLOOM_BATCH
-#define RM_BLOOM_BATCH 8
-#endif
-constexpr int kBloomBatch = RM_BLOOM_BATCH;
+// wave, not the arithmetic, bound a lone strip; 4 beat 8 by ~6%: fewer
+// registers, more waves).
+constexpr int kBloomBatch = 4;
 __global__ __launch_bounds__(256) void rm_bloom_min_kernel(const uint32_t* __restrict__ in, BloomPix B,
                                                            uint32_t* __restrict__ out, int W, int H) {
     const int x = blockIdx.x * 256 + threadIdx.x;
