@@ -67,10 +67,10 @@ def parse():
                          "split that gives rank 0 (which receives every other rank's rows and de-interleaves) "
                          "a longer run per cycle, sized from the timed exchange, and keeps whichever plan ran "
                          "the untimed trial frames faster")
-    ap.add_argument("--wire", default="rgb8", choices=["auto", "rgb8", "delta"],
-                    help="N > 1: the RGB8 wire (3 B/px, default), the compressed wire (DeltaFrame: a lossless "
-                         "delta code per 64-pixel row segment, 4-5x fewer bytes, DESIGN.md 4.4), or 'auto': both "
-                         "in the untimed trial, the faster timed")
+    ap.add_argument("--wire", default="auto", choices=["auto", "rgb8", "delta"],
+                    help="N > 1: the RGB8 wire (3 B/px), the compressed wire (DeltaFrame: the render kernel "
+                         "encodes its 8x8 tiles losslessly, ~7x fewer bytes on C3, DESIGN.md 4.4), or 'auto' "
+                         "(default): both in the untimed trial, the faster timed")
     ap.add_argument("--chunks", type=int, default=None,
                     help="render/gather chunks per frame (default 1: frames are pipelined instead)")
     ap.add_argument("--fmt", default="rgba8", choices=["rgba8", "float4"])
@@ -604,28 +604,39 @@ def main():
                 errors[name] = f"{type(e).__name__}: {e}"
                 torch.cuda.synchronize(dev)
 
+        def exchange(f):  # the even split's timed exchange, every rank's figures (collective)
+            xs = [f.timed_exchange() for _ in range(3)]
+            mine = torch.tensor([_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
+                                                                        "deinterleave_ms")],
+                                dtype=torch.float64, device=red_dev)
+            per = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(per, mine)
+            per = [[float(v) for v in x.cpu()] for x in per]
+            return {"render_ms": [x[0] for x in per], "pack_ms": [x[1] for x in per], "gather_ms": per[0][2],
+                    "deinterleave_ms": per[0][3]}
+
+        runs_delta, model_delta = None, None
         if args.wire in ("auto", "rgb8"):
             cands["even/rgb8"] = (fr, trial_ms(fr))
             if args.balance == "auto":
-                xs = [fr.timed_exchange() for _ in range(3)]
-                mine = torch.tensor([_median([x[k] for x in xs]) for k in ("render_ms", "pack_ms", "gather_ms",
-                                                                            "deinterleave_ms")],
-                                    dtype=torch.float64, device=red_dev)
-                per = [torch.empty_like(mine) for _ in range(world)]
-                dist.all_gather(per, mine)
-                per = [[float(v) for v in x.cpu()] for x in per]
-                ex = {"render_ms": [x[0] for x in per], "pack_ms": [x[1] for x in per], "gather_ms": per[0][2],
-                      "deinterleave_ms": per[0][3]}
-                runs, model = balanced_runs(world, args.band, H, ex)
+                runs, model = balanced_runs(world, args.band, H, exchange(fr))
                 build("balanced/rgb8", lambda: DistributedFrame(r, W, H, args.band, rank, world, fmt=args.fmt,
                                                                 chunks=chunks, streams=args.streams, runs=runs))
         if args.wire in ("auto", "delta"):
             build("even/delta", lambda: DeltaFrame(r, W, H, args.band, rank, world, streams=args.streams))
+            if args.balance == "auto" and "even/delta" in cands:
+                # the root renders rows and decodes every other part: its run
+                # sized from the compressed wire's own exchange
+                runs_delta, model_delta = balanced_runs(world, args.band, H, exchange(cands["even/delta"][0]))
+                if runs_delta != [args.band] * world:
+                    build("balanced/delta", lambda: DeltaFrame(r, W, H, args.band, rank, world,
+                                                               streams=args.streams, runs=runs_delta))
         chosen = min(cands, key=lambda k: cands[k][1])
         fr = cands[chosen][0]
         balance = {"mode": f"balance {args.balance}, wire {args.wire}", "chosen": chosen,
                    "runs": list(fr.plan.part_runs), "wire": fr.wire,
                    "trial_ms": {k: v[1] for k, v in cands.items()}, "balanced_runs": runs, "model": model,
+                   "balanced_runs_delta": runs_delta, "model_delta": model_delta,
                    "note": "untimed trial frames (16 pipelined frames per candidate, max over ranks) before the "
                            "instrumented run and the warm-up; the timed frames use the chosen candidate"}
         if errors:

@@ -34,11 +34,14 @@ __global__ __launch_bounds__(64) void rm_wire_tile_rows(const uint32_t* __restri
 
 // E2: one workgroup: the word counts of each 64-tile chunk (16 counts per
 // 16-byte load), an exclusive scan of the chunks into their bases (in the
-// workspace), the message size into the message and *size_out
+// workspace), the message size into the message and *size_out.  Thread t
+// sums chunks [t per, (t + 1) per); the thread sums are scanned per wave
+// (shuffles) and across the 16 waves (one barrier); a thread with one chunk
+// (every part of up to 65536 tiles) keeps its sum instead of reloading it.
 __global__ __launch_bounds__(1024) void rm_wire_tile_scan(const uint8_t* __restrict__ ws, long long T,
                                                           uint8_t* __restrict__ msg, long long* __restrict__ size_out) {
-    __shared__ unsigned long long part[1024];
-    const int t = threadIdx.x;
+    __shared__ uint32_t wave_total[16];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const uint8_t* counts = ws + wire_counts_offset(T);
     uint32_t* bases = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(ws) + wire_bases_offset(T));
     const long long C = wire_chunks(T), per = (C + 1023) / 1024, c0 = t * per, c1 = c0 + per < C ? c0 + per : C;
@@ -47,34 +50,44 @@ __global__ __launch_bounds__(1024) void rm_wire_tile_scan(const uint8_t* __restr
         uint32_t s = 0;
         if (i1 - i0 == 64 && ((reinterpret_cast<uintptr_t>(counts) + i0) & 15) == 0) {
             const uint4* q = reinterpret_cast<const uint4*>(counts + i0);
+            uint4 v[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint4 v = q[k];
-                for (uint32_t w : {v.x, v.y, v.z, v.w})  // four counts per word, each < 256
-                    s += (w & 255u) + ((w >> 8) & 255u) + ((w >> 16) & 255u) + (w >> 24);
-            }
+            for (int k = 0; k < 4; k++) v[k] = q[k];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                for (uint32_t x : {v[k].x, v[k].y, v[k].z, v[k].w})  // four counts per word, each < 256
+                    s += (x & 255u) + ((x >> 8) & 255u) + ((x >> 16) & 255u) + (x >> 24);
         } else {
             for (long long i = i0; i < i1; i++) s += counts[i];
         }
         return s;
     };
-    unsigned long long s = 0;
+    uint32_t s = 0;  // (the payload's words: < 2^27, the table's offset field)
     for (long long c = c0; c < c1; c++) s += chunk_sum(c);
-    part[t] = s;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the thread sums
-        const unsigned long long add = t >= o ? part[t - o] : 0ull;
-        __syncthreads();
-        part[t] += add;
-        __syncthreads();
+    uint32_t x = s;  // inclusive scan over the wave's lanes
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)x, k, 64);
+        if (l >= k) x += u;
     }
-    unsigned long long off = t > 0 ? part[t - 1] : 0ull;
-    for (long long c = c0; c < c1; c++) {
-        bases[c] = (uint32_t)off;
-        off += chunk_sum(c);
+    if (l == 63) wave_total[w] = x;
+    __syncthreads();
+    uint32_t off = x - s, total = 0;
+    for (int v = 0; v < 16; v++) {
+        const uint32_t wt = wave_total[v];
+        if (v < w) off += wt;
+        total += wt;
+    }
+    if (per == 1) {
+        if (c0 < C) bases[c0] = off;
+    } else {
+        for (long long c = c0; c < c1; c++) {
+            bases[c] = off;
+            off += chunk_sum(c);
+        }
     }
     if (t == 1023) {
-        const long long bytes = (long long)wire_header_bytes(T) + 8ll * (long long)part[1023];
+        const long long bytes = (long long)wire_header_bytes(T) + 8ll * (long long)total;
         *reinterpret_cast<long long*>(msg) = bytes;
         if (size_out) *size_out = bytes;
     }
@@ -113,10 +126,10 @@ __global__ __launch_bounds__(256) void rm_wire_tile_compact(const uint8_t* __res
     }
 }
 
-// D: a wave rebuilds 8 tiles (tx0 .. tx0 + 7 of tile row ty) of a part into
+// D: a wave rebuilds kDecodeTiles tiles (tx0 .. of tile row ty) of a part into
 // their pixels of the frame (the part's packed row j is frame row y(j): (y mod
-// cycle) - offset in [0, run)).  The 8 table entries and then every tile's
-// words are loaded before any is decoded (two memory round trips for the 8).
+// cycle) - offset in [0, run)).  The table entries and then every tile's words
+// are loaded before any is decoded (two memory round trips for the wave).
 // Lane l = pixel (l & 7, l >> 3) of a tile.
 //
 // Per tile, cross-lane work only on the VALU (no LDS): a bit plane is a
@@ -176,7 +189,7 @@ __device__ __forceinline__ uint32_t wire_decode_tile(uint64_t mine, int l) {
     return (va & 255u) | (((va >> 16) & 255u) << 8) | ((vb & 255u) << 16) | 0xFF000000u;
 }
 
-constexpr int kDecodeTiles = 8;  // tiles per wave
+constexpr int kDecodeTiles = 2;  // tiles per wave (1, 2, 4, 8 measured: 2 fastest, profiles/r06/decode_ab.log)
 constexpr int kDecodeWaves = 4;  // waves per workgroup (one-wave workgroups cap a CU's resident waves)
 __device__ __forceinline__ void wire_decode_tiles(const uint8_t* __restrict__ msg, int n, int W, int tx0, int ty,
                                                   int cycle, int offset, int run, uint32_t* __restrict__ frame) {
@@ -198,14 +211,19 @@ __device__ __forceinline__ void wire_decode_tiles(const uint8_t* __restrict__ ms
 #pragma unroll
     for (int k = 0; k < kDecodeTiles; k++) {
         if (k >= nt) break;
-        const uint32_t px = wire_decode_tile(mine[k], l);
+        // a flat tile (every width 0, about half of a rendered frame's): every
+        // pixel is the header's colour
+        const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mine[k]);
+        const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mine[k] >> 32));
+        const uint32_t px = ((h_lo >> 24) | (h_hi & 15u)) == 0 ? h_lo | 0xFF000000u : wire_decode_tile(mine[k], l);
         const int x = (tx0 + k) * 8 + (l & 7);
         if (x < W && j < n) frame[(size_t)y * W + x] = px;
     }
 }
 
-// D for several parts in one launch (grid ceil(TX / 32) x tile rows x parts,
-// wave w of a workgroup: tiles 8 (4 x + w) .. + 7 of the row)
+// D for several parts in one launch (grid ceil(TX / (kDecodeTiles
+// kDecodeWaves)) x tile rows x parts; wave w of workgroup x: tiles
+// kDecodeTiles (kDecodeWaves x + w) .. of the row)
 __global__ __launch_bounds__(64 * kDecodeWaves) void rm_wire_tile_decode_parts(WireParts parts, int W,
                                                                                uint32_t* __restrict__ frame) {
     const WirePart& P = parts.part[blockIdx.z];

@@ -62,15 +62,12 @@ __device__ __forceinline__ uint32_t wire_zigzag8(uint32_t d) {  // d mod 256 as 
     return (uint32_t)(s >= 0 ? 2 * s : -2 * s - 1);
 }
 
-// bit length of the wave maximum of z (0..8), wave-uniform: the highest set
-// bit of the lanes' OR, as ballots from the top
+// bit length of the wave maximum of z (0..8), wave-uniform: the least b with
+// every z < 2^b, one ballot per candidate from 0 up (b + 1 ballots: most
+// channels of a rendered tile are flat or one bit wide)
 __device__ __forceinline__ int wire_wave_width(uint32_t z) {
     int b = 0;
-    for (int i = 7; i >= 0; i--)
-        if (__builtin_amdgcn_ballot_w64((z >> i) & 1u)) {
-            b = i + 1;
-            break;
-        }
+    while (b < 8 && __builtin_amdgcn_ballot_w64((z >> b) != 0u)) b++;
     return b;
 }
 

@@ -106,6 +106,18 @@ def test_bench_two_ranks_gloo_compressed_wire(torch_cuda):
 
 
 @pytest.mark.gpu
+def test_bench_two_ranks_gloo_default_tries_both_wires(torch_cuda):
+    """The default (--balance auto --wire auto): the even and balanced RGB8
+    plans and the compressed wire all run untimed trial frames, the fastest
+    is timed, and its frame is bit-exact."""
+    res = _run(_torchrun(2, SMALL + ["--backend", "gloo"]))
+    b = res["balance"]
+    assert {"even/rgb8", "even/delta"} <= set(b["trial_ms"]), b
+    assert b["chosen"] == min(b["trial_ms"], key=b["trial_ms"].get) and res["wire"] == b["wire"], b
+    assert res["frame_check"]["result"] == "bit-exact", res
+
+
+@pytest.mark.gpu
 def test_bench_two_gpus_rccl(torch_cuda):
     """The same over RCCL, one rank per GPU (skipped below two GPUs)."""
     if torch_cuda.cuda.device_count() < 2:

@@ -21,6 +21,7 @@ timeout -k 10 300 python bench.py > $O/bench_C3.json 2> $O/bench_C3.err || { ech
 python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C3 ms/step', round(d['ms_per_step'],4), 'kernel', round(d['kernel_ms'],4), 'frac', d['roofline']['frac'], 'fxaa', round(d['post_pass']['ms'],4), 'bloom', round(d['bloom_pass']['ms'],4))" $O/bench_C3.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_C3 -o run -- python bench.py --cpu-seconds 0 > $O/bench_C3_under_rocprof.json 2> $O/bench_C3_under_rocprof.err || { echo "rocprof C3 failed"; exit 5; }
 find $O/trace_C3 -name "*kernel_stats.csv" -exec cp {} $O/bench_C3_kernel_stats.csv \;
+FRAME=random timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_fxaa_random -o run -- python tools/post_probe.py fxaa 4096 4096 20 > $O/trace_fxaa_random.log 2>&1 || { echo "fxaa noise trace failed"; exit 5; }
 timeout -k 10 300 python bench.py --scene O --size 8192 --max-steps 512 --steps 5 --warmup 2 --cpu-seconds 0 > $O/bench_C5frame.json 2> $O/bench_C5frame.err || { echo "bench C5 failed"; tail -20 $O/bench_C5frame.err; exit 6; }
 python -c "import json,sys; d=json.load(open(sys.argv[1])); print('C5 ms/step', round(d['ms_per_step'],4), 'kernel', round(d['kernel_ms'],4), 'frac', d['roofline']['frac'])" $O/bench_C5frame.json
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --backend gloo --cpu-seconds 0 > $O/bench_n2_gloo.json 2> $O/bench_n2_gloo.err || { echo "gloo N=2 failed"; tail -20 $O/bench_n2_gloo.err; exit 7; }
@@ -31,5 +32,6 @@ if [ "${PMC:-0}" = 1 ]; then
   bash tools/pmc_post.sh fxaa && mv gpurun_out/pmc_fxaa $O/pmc_fxaa || exit 10
   bash tools/pmc_post.sh bloom && mv gpurun_out/pmc_bloom $O/pmc_bloom || exit 11
   bash tools/pmc_post.sh post_chain && mv gpurun_out/pmc_post_chain $O/pmc_post_chain || exit 12
+  FRAME=random bash tools/pmc_post.sh fxaa && mv gpurun_out/pmc_fxaa_random $O/pmc_fxaa_random || exit 13
 fi
 echo "validate $TAG done"

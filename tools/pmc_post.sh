@@ -1,9 +1,10 @@
 # PMC passes (one rocprofv3 run per counter group) over tools/post_probe.py.
-# Usage: bash tools/pmc_post.sh fxaa|bloom|post_chain ; summaries via tools/pmc_parse.py
+# Usage: [FRAME=random] bash tools/pmc_post.sh fxaa|bloom|post_chain ; summaries via
+# tools/pmc_parse.py -> gpurun_out/pmc_<which>[_random]/summary.json
 set -u
 export TMPDIR=/tmp
 P=${1:-fxaa}
-D=gpurun_out/pmc_$P
+D=gpurun_out/pmc_$P${FRAME:+_$FRAME}
 mkdir -p $D
 i=0
 while read -r G; do

@@ -1,7 +1,8 @@
 """Post-pass driver for rocprofv3 runs: one 4096^2 scene-T RGBA8 frame, then
 `reps` passes of `fxaa`, `bloom` or `post_chain` (FXAA then bloom of its
-output, rm_post_chain) over it (tools/; not part of the product).
-Usage: post_probe.py fxaa|bloom|post_chain|fxaa_bloom [W] [H] [reps]"""
+output, rm_post_chain) over it (tools/; not part of the product).  FRAME=random
+replaces the rendered frame by uniform noise (FXAA's worst content: no short
+spans).  Usage: post_probe.py fxaa|bloom|post_chain|fxaa_bloom [W] [H] [reps]"""
 import os
 import sys
 
@@ -19,6 +20,9 @@ r.load_scene("template.frag")
 r.set_pose(*[rm.POSES["P0"][k] for k in ("pos", "mouse", "time")])
 r.set_params(max_steps=256, count_evals=0)
 frame = r.render_rgba8(W, H)
+if os.environ.get("FRAME") == "random":
+    g = torch.Generator(device="cuda").manual_seed(7)
+    frame = torch.randint(-2**31, 2**31 - 1, (H, W), dtype=torch.int32, device="cuda", generator=g)
 out = torch.empty_like(frame)
 mid = torch.empty_like(frame)
 for _ in range(reps):

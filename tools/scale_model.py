@@ -17,9 +17,11 @@ gather_ms).  Both the even split (bands of 16) and bench.py's balanced split
 --wire delta models the compressed wire (DeltaFrame) instead:
 every non-root rank renders straight into its message
 (rm_render_cycle_rows_wire, the encode in the render kernel's epilogue, plus
-the scan and compaction), the root renders its rows and copies them into the
-frame, then decodes the other parts' messages (one rm_wire_decode_parts
-launch, timed alone on their real messages); the link carries the messages.
+the scan and compaction), the root renders its rows, copies them into the
+frame and decodes the other parts' real messages (their last frame's, one
+rm_wire_decode_parts launch) in the same two-stream frame loop, so the
+decode overlaps the next frame's render as in DeltaFrame (the decode alone is
+also timed, root_decode_ms); the link carries the messages.
 
 Usage: scale_model.py [--config C3|C5] [--ns 1,2,4,8] [--frames 24] [--link-gbs 64] [--wire rgb8|delta]
 One JSON line per (N, split)."""
@@ -91,9 +93,13 @@ def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
             if not delta:
                 r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[k])
                 r.pack_rgb8(loc[k], out=wire[k])
-            elif rank == 0:  # its rows into the frame (the decode of the others is timed apart)
+            elif rank == 0:  # its rows into the frame, then the other parts' messages decoded into it
                 r.render_cycle_rows(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, loc[k])
                 r.scatter_part_rgba8(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], n, loc[k], frame)
+                if len(MESSAGES) == p.nshards - 1:
+                    qs = range(1, p.nshards)
+                    r.wire_decode_parts(W, p.H, p.cycle, [p.offsets[q] for q in qs], [p.part_runs[q] for q in qs],
+                                        [MESSAGES[q][1] for q in qs], [MESSAGES[q][0] for q in qs], frame)
             else:
                 r.render_cycle_rows_wire(W, p.H, p.cycle, p.offsets[rank], p.part_runs[rank], 0, n, msg[k], ws[k],
                                          size[k])
@@ -124,9 +130,18 @@ def per_frame_ms(r, torch, plan, rank, frames, nstreams=2):
 MESSAGES = {}  # rank -> (message, rows) of the last modelled plan (--wire delta)
 
 
+def per_rank(r, torch, plan, args):
+    """Every rank's per_frame_ms; with the compressed wire the other ranks
+    first, so that the root's frames decode their messages."""
+    order = list(range(1, plan.nshards)) + [0] if WIRE == "delta" else list(range(plan.nshards))
+    out = {q: per_frame_ms(r, torch, plan, q, args.frames, args.streams) for q in order}
+    return [out[q] for q in range(plan.nshards)]
+
+
 def decode_ms(r, torch, plan):
     """The root's decode of every other part's message into the frame (one launch)."""
     W, H = plan.W, plan.H
+    r.set_stream(torch.cuda.current_stream())  # (the frame loop left a frame stream bound: time on the events' one)
     frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
     qs = list(range(1, plan.nshards))
     args = (W, H, plan.cycle, [plan.offsets[q] for q in qs], [plan.part_runs[q] for q in qs],
@@ -144,6 +159,7 @@ def decode_ms(r, torch, plan):
 
 def deinterleave_ms(r, torch, plan):
     W, H = plan.W, plan.H
+    r.set_stream(torch.cuda.current_stream())
     g = torch.randint(0, 255, (H, 3 * W), dtype=torch.uint8, device="cuda")
     out = torch.empty((H, W), dtype=torch.int32, device="cuda")
     bases = [b * 3 * W for b in plan.part_bases()]
@@ -194,29 +210,39 @@ def main():
     for N in [int(x) for x in args.ns.split(",")]:
         even = ShardPlan(W, H, args.band if N > 1 else H, N, None if N > 1 else (H,))
         MESSAGES.clear()
-        per = [per_frame_ms(r, torch, even, q, args.frames, args.streams) for q in range(N)]
+        per = per_rank(r, torch, even, args)
         d = (decode_ms(r, torch, even) if args.wire == "delta" else deinterleave_ms(r, torch, even)) if N > 1 else 0.0
         wire_even = ([0] + [int(MESSAGES[q][0].numel()) for q in range(1, N)] if args.wire == "delta" and N > 1
                      else None)
-        rows = {"even": (even, per, d)}
-        if N > 1 and not args.even_only and args.wire == "rgb8":
-            ex = {"render_ms": [x[0] for x in per], "gather_ms": max(even.count(q) for q in range(1, N)) * 3 * W
-                  / link_bpms, "deinterleave_ms": d}
+        rows = {"even": (even, per, d, wire_even)}
+        if N > 1 and not args.even_only:
+            # the root's run sized so that its rows plus the decode (or de-interleave)
+            # take as long as another rank's rows or its link time (bench.balanced_runs)
+            gbytes = max(wire_even[1:]) if wire_even else max(even.count(q) for q in range(1, N)) * 3 * W
+            ex = {"render_ms": [x[0] for x in per], "gather_ms": gbytes / link_bpms, "deinterleave_ms": d}
             runs, model = balanced_runs(N, args.band, H, ex)
-            bal = ShardPlan(W, H, args.band, N, tuple(runs))
-            perb = [per_frame_ms(r, torch, bal, q, args.frames, args.streams) for q in range(N)]
-            rows["balanced"] = (bal, perb, deinterleave_ms(r, torch, bal))
-        for name, (plan, pr, dms) in rows.items():
-            wire = wire_even if wire_even is not None else [plan.count(q) * 3 * W for q in range(N)]
+            if tuple(runs) != tuple(even.part_runs):
+                bal = ShardPlan(W, H, args.band, N, tuple(runs))
+                MESSAGES.clear()
+                perb = per_rank(r, torch, bal, args)
+                if args.wire == "delta":
+                    rows["balanced"] = (bal, perb, decode_ms(r, torch, bal),
+                                        [0] + [int(MESSAGES[q][0].numel()) for q in range(1, N)])
+                else:
+                    rows["balanced"] = (bal, perb, deinterleave_ms(r, torch, bal), None)
+        for name, (plan, pr, dms, wire) in rows.items():
+            wire = wire if wire is not None else [plan.count(q) * 3 * W for q in range(N)]
             link = max(wire[1:], default=0) / link_bpms
-            compute = [pr[0][0] + dms] + [x[0] for x in pr[1:]]
+            # (with the compressed wire the root's frames already decode the others' messages)
+            compute = [pr[0][0] + (dms if args.wire == "rgb8" else 0.0)] + [x[0] for x in pr[1:]]
             frame = max(max(compute), link)
             print(json.dumps({
                 "config": args.config, "N": N, "split": name, "wire": args.wire, "streams": args.streams,
                 "stream_kind": args.stream_kind, "runs": list(plan.part_runs),
                 "per_rank_frame_ms": [round(x[0], 4) for x in pr],
                 "per_rank_kernel_ms": [round(x[1], 4) for x in pr],
-                ("root_decode_ms" if args.wire == "delta" else "deinterleave_ms"): round(dms, 4), "wire_bytes": wire,
+                ("root_decode_ms" if args.wire == "delta" else "deinterleave_ms"): round(dms, 4),
+                "root_frame_includes_decode": args.wire == "delta", "wire_bytes": wire,
                 "link_gbs_assumed": args.link_gbs,
                 "link_ms": round(link, 4), "projected_frame_ms": round(frame, 4),
                 "bound": "link" if link >= max(compute) else ("root" if compute[0] >= max(compute[1:], default=0)
