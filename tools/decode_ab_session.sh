@@ -1,3 +1,4 @@
+# Decode A/B session (tools/decode_ab.py under a kernel trace, per variant library in raymarching_amd/variants/, two passes).
 set -u
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
