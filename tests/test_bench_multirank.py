@@ -63,6 +63,10 @@ def test_bench_one_gpu_frame_check(torch_cuda, scene):
     assert res["n_gpus"] == 1 and "gather_ms" not in res
     _check_roofline(res)
     assert res["roofline"]["frac"] is None  # no counters for a 512x512 frame
+    # the reference's whole frame (render -> FXAA -> bloom of the FXAA frame),
+    # its post chain checked against rm_fxaa then rm_bloom
+    assert res["pipeline"]["chain_check"]["result"] == "bit-exact", res["pipeline"]
+    assert res["pipeline_ms"] > res["ms_per_step"] * 0.9, res
 
 
 @pytest.mark.gpu
