@@ -150,22 +150,31 @@ template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
 __device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // DPP move; disabled and out-of-row lanes read 0
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, BANK_MASK, true);
 }
-__device__ __forceinline__ uint32_t wire_decode_tile(uint64_t mine, int l) {
-    const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mine);
-    const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mine >> 32));
-    const int b[3] = {min((int)((h_lo >> 24) & 15u), 8), min((int)(h_lo >> 28), 8), min((int)(h_hi & 15u), 8)};
+// Plane q (payload word q = 1 .. nq) gives bit q - 1 of a lane's `bits`, all
+// planes in one fully unrolled gather (constant lane indices, no scalar loop
+// per plane); a channel's z is then a field of `bits`.  Words past the tile's
+// count were loaded as 0, so planes past nq add nothing.
+__device__ __forceinline__ uint32_t wire_decode_tile(uint64_t mine, int l, uint32_t h_lo, uint32_t h_hi) {
+    const int bR = min((int)((h_lo >> 24) & 15u), 8), bG = min((int)(h_lo >> 28), 8), bB = min((int)(h_hi & 15u), 8);
+    const int nq = bR + bG + bB;
     const uint32_t m_lo = (uint32_t)mine, m_hi = (uint32_t)(mine >> 32);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int g = 0; g < 3 * 8; g += 4) {
+        if (g >= nq) break;  // (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t plane = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m_lo, 1 + g + k) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m_hi, 1 + g + k) << 32);
+            bits |= lane_bit(plane) << (g + k);
+        }
+    }
+    const uint32_t z[3] = {bits & ((1u << bR) - 1u), (bits >> bR) & ((1u << bG) - 1u),
+                           (bits >> (bR + bG)) & ((1u << bB) - 1u)};
     uint32_t d[3];
-    int q = 1;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-        uint32_t z = 0;
-        for (int i = 0; i < b[c]; i++, q++) {
-            const uint64_t plane = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m_lo, q) |
-                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m_hi, q) << 32);
-            z |= lane_bit(plane) << i;
-        }
-        const int s = (int)(z >> 1) ^ -(int)(z & 1u);  // zig-zag back: the difference as int8
+        const int s = (int)(z[c] >> 1) ^ -(int)(z[c] & 1u);  // zig-zag back: the difference as int8
         d[c] = l == 0 ? (h_lo >> (8 * c)) & 255u : (uint32_t)s & 255u;
     }
     // the sums mod 256 per channel, two channels per word in 16-bit fields (at
@@ -215,7 +224,8 @@ __device__ __forceinline__ void wire_decode_tiles(const uint8_t* __restrict__ ms
         // pixel is the header's colour
         const uint32_t h_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mine[k]);
         const uint32_t h_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mine[k] >> 32));
-        const uint32_t px = ((h_lo >> 24) | (h_hi & 15u)) == 0 ? h_lo | 0xFF000000u : wire_decode_tile(mine[k], l);
+        const uint32_t px =
+            ((h_lo >> 24) | (h_hi & 15u)) == 0 ? h_lo | 0xFF000000u : wire_decode_tile(mine[k], l, h_lo, h_hi);
         const int x = (tx0 + k) * 8 + (l & 7);
         if (x < W && j < n) frame[(size_t)y * W + x] = px;
     }

@@ -2,7 +2,8 @@
 frame: every non-root part of an even N-rank split encoded by the render
 epilogue, then all of them decoded into the frame in one launch, timed with
 events on the stream the renderer is bound to; the frame is checked against
-rm_render_rgba8.  One JSON line per N.  Run once per library (RM_LIB=...).
+rm_render_rgba8.  One JSON line per N (DEC_NS, default 2,8).  Run once per
+library (RM_LIB=...).
 (tools/; not product.)"""
 import json
 import os
@@ -23,7 +24,7 @@ p = rm.POSES["P0"]
 r.set_pose(p["pos"], p["mouse"], p["time"])
 r.set_params(max_steps=256, count_evals=0, schedule=1)
 ref = r.render_rgba8(W, H)
-for N in (2, 8):
+for N in [int(x) for x in os.environ.get("DEC_NS", "2,8").split(",")]:
     plan = ShardPlan(W, H, 16, N)
     frame = torch.zeros((H, W), dtype=torch.int32, device="cuda")
     msgs = []
