@@ -351,7 +351,8 @@ def time_pipeline(r, W, H, stream, counters, render_ms, reps=20):
     pipeline_ms = event interval per frame; post_chain = the two post passes
     alone; chain_check: rm_post_chain's output against rm_fxaa then rm_bloom of
     the same frame (GPU, bit for bit; tests/test_post_chain.py holds the
-    oracle's chain)."""
+    oracle's chain).  Untimed frames for 0.3 s first, as before the timed
+    frames."""
     import torch
 
     frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
@@ -361,8 +362,11 @@ def time_pipeline(r, W, H, stream, counters, render_ms, reps=20):
         r.render_rgba8(W, H, out=frame)
         r.post_chain(frame, mid=mid, out=out)
 
-    for _ in range(3):
+    import time
+    t_end = time.time() + 0.3  # spin-up as for the timed frames: the GPU's clocks settle to the mixed load
+    while time.time() < t_end:
         step()
+        stream.synchronize()
     pipe_ms = _timed(stream, reps, step)
     chain_ms = _timed(stream, reps, lambda: r.post_chain(frame, mid=mid, out=out))
     ref = r.bloom(r.fxaa(frame))
