@@ -200,6 +200,28 @@ def concurrent_streams(dev, n, tries=12):
     return chosen
 
 
+class _OnStream:
+    """`with torch.cuda.stream(st)` for a stream of a known device, without the
+    current-device queries of torch's StreamContext (a frame at N = 8 is
+    ~0.08 ms of GPU time: the multi-GPU loops' host time per frame has to stay
+    below that; tools/host_overhead_probe.py)."""
+    __slots__ = ("st", "prev")
+
+    def __init__(self, st):
+        self.st = st
+
+    def __enter__(self):
+        import torch
+        self.prev = torch.cuda.current_stream(self.st.device)
+        torch.cuda.set_stream(self.st)
+        return self.st
+
+    def __exit__(self, *exc):
+        import torch
+        torch.cuda.set_stream(self.prev)
+        return False
+
+
 class DistributedFrame:
     """One rank's share of a row-sharded frame on its GPU.
 
@@ -305,6 +327,67 @@ class DistributedFrame:
         self.frame = self.frames[0] if self.frames is not None else None
         self.k = 0            # frames submitted
         self.pending = None   # (slot, stream, [works]) of the frame whose gather is in flight
+        self._pipe = self._pipelined()
+        self._prepare_calls()
+
+    def _prepare_calls(self):
+        """The per-frame native calls of submit() with their arguments built
+        once per slot and chunk (render, RGB8 pack, the root's de-interleave):
+        the Python wrappers' checks cost as much host time as a rank's frame
+        takes on the GPU at N = 8."""
+        import ctypes
+
+        import torch
+
+        from ._lib import lib
+        L, p, ctx = lib(), self.plan, self.r._ctx
+        rgba8 = self.fmt == "rgba8"
+
+        def vp(t):
+            return ctypes.c_void_p(t.data_ptr())
+
+        self._render_calls, self._pack_calls, self._deint_calls = [], [], []
+        for slot in range(len(self.wires)):
+            dst = self.wires[slot] if self.locals is None else self.locals[slot]
+            rc, pc = [], []
+            for c in range(len(self.cuts) - 1):
+                j0, j1 = self.cuts[c], min(self.cuts[c + 1], self.nmine)
+                if j1 <= j0:
+                    rc.append(None)
+                    pc.append(None)
+                    continue
+                if p.weighted:
+                    fn = L.rm_render_cycle_rows_rgba8 if rgba8 else L.rm_render_cycle_rows
+                    args = (ctx, p.W, p.H, p.cycle, p.offsets[self.rank], p.part_runs[self.rank], j0, j1 - j0,
+                            vp(dst[j0:j1]), None)
+                else:
+                    fn = L.rm_render_rows_rgba8 if rgba8 else L.rm_render_rows
+                    args = (ctx, p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, vp(dst[j0:j1]), None)
+                rc.append((fn, args))
+                pc.append((L.rm_pack_rgb8, (ctx, (j1 - j0) * p.W, vp(self.locals[slot][j0:j1]),
+                                            vp(self.wires[slot][j0:j1]))) if self.locals is not None else None)
+            self._render_calls.append(rc)
+            self._pack_calls.append(pc)
+            d = None
+            if self.rank == 0 and self.world > 1 and self.gathered is not None:
+                g, f = self.gathered[slot], self.frames[slot]
+                if p.weighted:
+                    n = p.nshards
+                    d = (L.rm_deinterleave_cycle_rgb8,
+                         (ctx, p.W, p.H, p.cycle, n, (ctypes.c_int * n)(*p.offsets), (ctypes.c_int * n)(*p.part_runs),
+                          (ctypes.c_int64 * n)(*[b * 3 * p.W for b in p.part_bases()]), vp(g), vp(f)))
+                elif g.dtype == torch.uint8:
+                    d = (L.rm_deinterleave_rgb8, (ctx, p.W, p.H, p.band, p.nshards, p.rows_per_shard, vp(g), vp(f)))
+                else:
+                    fn = L.rm_deinterleave_rgba8 if rgba8 else L.rm_deinterleave
+                    d = (fn, (ctx, p.W, p.H, p.band, p.nshards, p.rows_per_shard, vp(g), vp(f)))
+            self._deint_calls.append(d)
+
+    def _native(self, call):
+        from ._lib import check
+        rc = call[0](*call[1])
+        if rc:
+            check(rc, self.r._ctx)
 
     def _pipelined(self):
         import torch.distributed as dist
@@ -318,18 +401,19 @@ class DistributedFrame:
                                             j1 - j0, dst[j0:j1], stats=stats)
         return self.r.render_rows(p.W, p.H, p.band, p.nshards, self.rank, j0, j1 - j0, dst[j0:j1], stats=stats)
 
-    def _render_rows(self, j0, j1, slot, events=None):
-        j1 = min(j1, self.nmine)
-        if j1 <= j0:
+    def _render_rows(self, c, slot, events=None, st=None):
+        """Chunk c of this rank's rows into slot `slot` (and packed to RGB8), on
+        the current stream st."""
+        call = self._render_calls[slot][c]
+        if call is None:
             return
-        dst = self.wires[slot] if self.locals is None else self.locals[slot]
         if events is not None:
-            events[0].record()
-        self._render_into(dst, j0, j1)
+            events[0].record(st)
+        self._native(call)
         if events is not None:
-            events[1].record()
-        if self.locals is not None:
-            self.r.pack_rgb8(self.locals[slot][j0:j1], out=self.wires[slot][j0:j1])
+            events[1].record(st)
+        if self._pack_calls[slot][c] is not None:
+            self._native(self._pack_calls[slot][c])
 
     def _gather_async(self, slot, c):
         """Start chunk c's gather (c None: every row); returns the works."""
@@ -409,13 +493,13 @@ class DistributedFrame:
         self.k += 1
         nch = len(self.cuts) - 1
         works = []
-        with torch.cuda.stream(st):  # the collectives order themselves after this stream
+        with _OnStream(st):  # the collectives order themselves after this stream
             self._bind(st)
             for c in range(nch):
-                self._render_rows(self.cuts[c], self.cuts[c + 1], slot, None if events is None else events[c])
-                if self._pipelined():
+                self._render_rows(c, slot, None if events is None else events[c], st)
+                if self._pipe:
                     works.extend(self._gather_async(slot, c))
-            if self.world > 1 and not self._pipelined():  # gloo: one host-staged gather, completed here
+            if self.world > 1 and not self._pipe:  # gloo: one host-staged gather, completed here
                 self._gather_blocking(slot)
                 works = None
         self.r.set_stream(self.caller)
@@ -430,12 +514,12 @@ class DistributedFrame:
         import torch
 
         slot, st, works = item
-        with torch.cuda.stream(st):
+        with _OnStream(st):
             self._bind(st)
             for w in works or ():
                 w.wait()  # st waits for the gather
             if self.rank == 0:
-                self._deinterleave(slot)
+                self._native(self._deint_calls[slot])
                 self.frame = self.frames[slot]
         self.r.set_stream(self.caller)
 
@@ -589,6 +673,7 @@ class DeltaFrame(DistributedFrame):
         self.pending = None
         self.last_sizes = [0] * world
         self.fused = rank != 0  # (the render kernel encodes; scene plugins fall back, _render_message)
+        self._pipe = self._pipelined()
         # the per-frame native calls with their arguments built once (a frame
         # at N = 8 is ~0.1 ms: Python-side argument checks per call would cost
         # as much as the GPU work)
@@ -597,6 +682,16 @@ class DeltaFrame(DistributedFrame):
         from ._lib import lib
         self._L = lib()
         if rank == 0:
+            # the root's own rows (as _render_into, its arguments built once)
+            vp = ctypes.c_void_p
+            if p.weighted:
+                self._root_render = [(self._L.rm_render_cycle_rows_rgba8,
+                                      (renderer._ctx, W, H, p.cycle, p.offsets[0], p.part_runs[0], 0, self.nmine,
+                                       vp(t.data_ptr()), None)) for t in self.locals]
+            else:
+                self._root_render = [(self._L.rm_render_rows_rgba8,
+                                      (renderer._ctx, W, H, p.band, p.nshards, 0, 0, self.nmine, vp(t.data_ptr()),
+                                       None)) for t in self.locals]
             qs = list(range(1, world))
             self._dec = [((ctypes.c_int * len(qs))(*[p.offsets[q] for q in qs]),
                           (ctypes.c_int * len(qs))(*[p.part_runs[q] for q in qs]),
@@ -622,7 +717,7 @@ class DeltaFrame(DistributedFrame):
         from ._lib import RmError, RmStats
         p, q = self.plan, self.rank
         if self.fused:
-            s = RmStats()
+            s = RmStats() if stats else None
             try:
                 self._call(self._L.rm_render_cycle_rows_wire(
                     self.r._ctx, p.W, p.H, p.cycle, p.offsets[q], p.part_runs[q], 0, self.nmine,
@@ -650,7 +745,7 @@ class DeltaFrame(DistributedFrame):
         copy them into the frame or (others) encode them."""
         import torch
         p = self.plan
-        with torch.cuda.stream(st):
+        with _OnStream(st):
             self._bind(st)
             for w in self.slot_works[slot]:  # the slot's previous message has left
                 w.wait()
@@ -659,7 +754,7 @@ class DeltaFrame(DistributedFrame):
                 events[0].record()
             if self.rank == 0:
                 if self.nmine:
-                    self._render_into(self.locals[slot], 0, self.nmine)
+                    self._call(self._root_render[slot][0](*self._root_render[slot][1]))
                 if events is not None:
                     events[1].record()
                 self._scatter(slot)
@@ -682,8 +777,8 @@ class DeltaFrame(DistributedFrame):
         else:
             self.size_ev[slot].synchronize()  # the encoder's size has reached the host
             mine = int(self.size_host[slot][0])
-        if self._pipelined():
-            with torch.cuda.stream(self.ctrl):
+        if self._pipe:
+            with _OnStream(self.ctrl):
                 sz = torch.full((1,), mine, dtype=torch.int64, device=self.dev)
                 allsz = torch.empty(self.world, dtype=torch.int64, device=self.dev)
                 dist.all_gather_into_tensor(allsz, sz, group=self.group)
@@ -735,7 +830,7 @@ class DeltaFrame(DistributedFrame):
         sizes, works = self._sizes_and_messages(slot)
         self.last_sizes = sizes
         if self.rank == 0:
-            with torch.cuda.stream(st):
+            with _OnStream(st):
                 self._bind(st)
                 for w in works:
                     w.wait()
@@ -753,7 +848,7 @@ class DeltaFrame(DistributedFrame):
         self.k += 1
         self._produce(slot, st, None if events is None else events[0])
         prev, self.pending = self.pending, (slot, st)
-        if not self._pipelined():
+        if not self._pipe:
             self.pending = None
             self._exchange(slot, st)
         elif prev is not None:
