@@ -674,6 +674,8 @@ class DeltaFrame(DistributedFrame):
         self.last_sizes = [0] * world
         self.fused = rank != 0  # (the render kernel encodes; scene plugins fall back, _render_message)
         self._pipe = self._pipelined()
+        self._zero_size = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._allsz = [torch.zeros(world, dtype=torch.int64, device=dev) for _ in range(nbuf)]
         # the per-frame native calls with their arguments built once (a frame
         # at N = 8 is ~0.1 ms: Python-side argument checks per call would cost
         # as much as the GPU work)
@@ -779,10 +781,11 @@ class DeltaFrame(DistributedFrame):
             mine = int(self.size_host[slot][0])
         if self._pipe:
             with _OnStream(self.ctrl):
-                sz = torch.full((1,), mine, dtype=torch.int64, device=self.dev)
-                allsz = torch.empty(self.world, dtype=torch.int64, device=self.dev)
-                dist.all_gather_into_tensor(allsz, sz, group=self.group)
-                sizes = [int(v) for v in allsz.cpu()]
+                # (the encoder's device size, complete once size_ev was reached;
+                # preallocated buffers: no allocation or fill per frame)
+                src = self.size_dev[slot] if self.rank else self._zero_size
+                dist.all_gather_into_tensor(self._allsz[slot], src, group=self.group)
+                sizes = self._allsz[slot].tolist()
                 self._check_sizes(sizes)  # (every rank: all fail together, before any send or receive)
                 if self.rank == 0:
                     if self.decoded_recorded[slot]:

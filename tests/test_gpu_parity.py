@@ -1054,6 +1054,100 @@ def test_compressed_wire_pipelined_in_one_process(R, torch_cuda, runs):
     r1.close()
 
 
+@pytest.mark.parametrize("runs", [None, (13, 8)])
+def test_compressed_wire_rccl_exchange_code_in_one_process(R, torch_cuda, runs, monkeypatch):
+    """DeltaFrame's own RCCL exchange code (_sizes_and_messages with the size
+    all-gather on the control stream and the point-to-point messages, as the
+    "nccl" backend runs it), two ranks in one process: only the three
+    torch.distributed calls it makes are replaced by in-process equivalents
+    (all_gather_into_tensor of the device sizes, P2POp, batch_isend_irecv with
+    works whose wait() orders the caller's stream).  Every frame equals
+    rm_render_rgba8's."""
+    torch = torch_cuda
+    import torch.distributed as dist
+    from raymarching_amd.frame import DeltaFrame
+    W, H, band = 96, 70, 8
+    side = torch.cuda.Stream()
+    gathered, sent = {}, {}
+
+    class Work:
+        def __init__(self, ev=None, entry=None):
+            self.ev, self.entry = ev, entry
+
+        def wait(self):  # the caller's stream waits for the transfer
+            ev = self.ev if self.ev is not None else (self.entry or {}).get("done")
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+
+    def all_gather_into_tensor(out, inp, group=None):
+        # rank 1 (submitted first in each frame) brings its message size, the
+        # root 0; both receive [0, size of rank 1]
+        v = int(inp.item())
+        if v:
+            gathered["r1"] = v
+        out.copy_(torch.tensor([0, gathered["r1"]], dtype=torch.int64, device=out.device))
+
+    class P2POp:
+        def __init__(self, op, tensor, peer, group=None):
+            self.op, self.tensor, self.peer = op, tensor, peer
+
+    def batch_isend_irecv(ops):
+        works = []
+        for o in ops:
+            if o.op is dist.isend:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream())
+                entry = {"src": o.tensor, "ev": ev}
+                sent["msg"] = entry
+                works.append(Work(entry=entry))  # (the sender's buffer is free once the copy is done)
+            else:
+                entry = sent.pop("msg")
+                assert entry["src"].numel() == o.tensor.numel()
+                side.wait_stream(torch.cuda.current_stream())
+                side.wait_event(entry["ev"])
+                with torch.cuda.stream(side):
+                    o.tensor.copy_(entry["src"])
+                done = torch.cuda.Event()
+                done.record(side)
+                entry["done"] = done
+                works.append(Work(ev=done))
+        return works
+
+    monkeypatch.setattr(dist, "all_gather_into_tensor", all_gather_into_tensor)
+    monkeypatch.setattr(dist, "P2POp", P2POp)
+    monkeypatch.setattr(dist, "batch_isend_irecv", batch_isend_irecv)
+    r1 = rm.Renderer(0)
+    frs = []
+    for rank, rr in ((0, R), (1, r1)):
+        f = DeltaFrame.__new__(DeltaFrame)
+        f._pipelined = lambda: True  # as with the "nccl" backend
+        DeltaFrame.__init__(f, rr, W, H, band, rank, 2, runs=runs)
+        frs.append(f)
+    poses = ["P0", "P1", "P2", "P3"]
+    refs = []
+    for name in poses:
+        setup(R, "T", POSES[name], 128)
+        R.set_params(count_evals=0)
+        refs.append(R.render_rgba8(W, H).cpu().numpy())
+    got = []
+    for i, name in enumerate(poses):
+        for f, rr in ((frs[1], r1), (frs[0], R)):
+            setup(rr, "T", POSES[name], 128)
+            rr.set_params(count_evals=0)
+            f.submit()
+        if i > 0:
+            torch.cuda.synchronize()
+            got.append(frs[0].frame.cpu().numpy())
+    frs[1].flush()
+    got.append(frs[0].flush().cpu().numpy())
+    torch.cuda.synchronize()
+    assert len(got) == len(refs)
+    for g, ref in zip(got, refs):
+        assert np.array_equal(g, ref)
+    assert frs[0].last_sizes[0] == 0 and frs[0].last_sizes[1] > 0
+    r1.close()
+
+
 def test_context_outlives_a_destroyed_stream(torch_cuda):
     """Completion events are recorded lazily: when the
     context leaves a stream, the event goes on that stream while it still
