@@ -1148,6 +1148,109 @@ def test_compressed_wire_rccl_exchange_code_in_one_process(R, torch_cuda, runs, 
     r1.close()
 
 
+@pytest.mark.parametrize("runs", [None, (13, 8)])
+def test_rgb8_rccl_gather_code_in_one_process(R, torch_cuda, runs, monkeypatch):
+    """DistributedFrame's own RCCL gather code (_gather_async: the async
+    ncclGather of equal bands, or the unpadded point-to-point parts, as the
+    "nccl" backend runs them), two ranks in one process with only
+    dist.gather / P2POp / batch_isend_irecv replaced by in-process device
+    copies whose works order the caller's stream.  Every frame equals
+    rm_render_rgba8's."""
+    torch = torch_cuda
+    import torch.distributed as dist
+    from raymarching_amd.frame import DistributedFrame
+    W, H, band = 96, 70, 8
+    side = torch.cuda.Stream()
+    pending = {}
+
+    class Work:
+        def __init__(self, ev=None, entry=None):
+            self.ev, self.entry = ev, entry
+
+        def wait(self):
+            ev = self.ev if self.ev is not None else (self.entry or {}).get("done")
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+
+    def copy_after(dst, src, ev):
+        side.wait_stream(torch.cuda.current_stream())
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            dst.copy_(src)
+
+    def gather(tensor, gather_list=None, dst=0, group=None, async_op=False):
+        assert async_op and dst == 0
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        if gather_list is None:  # rank 1 (submitted first)
+            entry = {"src": tensor, "ev": ev}
+            pending["gather"] = entry
+            return Work(entry=entry)
+        entry = pending.pop("gather")
+        copy_after(gather_list[0], tensor, ev)
+        copy_after(gather_list[1], entry["src"], entry["ev"])
+        done = torch.cuda.Event()
+        done.record(side)
+        entry["done"] = done
+        return Work(ev=done)
+
+    class P2POp:
+        def __init__(self, op, tensor, peer, group=None):
+            self.op, self.tensor, self.peer = op, tensor, peer
+
+    def batch_isend_irecv(ops):
+        works = []
+        for o in ops:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            if o.op is dist.isend:
+                entry = {"src": o.tensor, "ev": ev}
+                pending["p2p"] = entry
+                works.append(Work(entry=entry))
+            else:
+                entry = pending.pop("p2p")
+                assert entry["src"].numel() == o.tensor.numel()
+                copy_after(o.tensor, entry["src"], entry["ev"])
+                done = torch.cuda.Event()
+                done.record(side)
+                entry["done"] = done
+                works.append(Work(ev=done))
+        return works
+
+    monkeypatch.setattr(dist, "gather", gather)
+    monkeypatch.setattr(dist, "P2POp", P2POp)
+    monkeypatch.setattr(dist, "batch_isend_irecv", batch_isend_irecv)
+    r1 = rm.Renderer(0)
+    frs = []
+    for rank, rr in ((0, R), (1, r1)):
+        f = DistributedFrame.__new__(DistributedFrame)
+        f._pipelined = lambda: True  # as with the "nccl" backend
+        DistributedFrame.__init__(f, rr, W, H, band, rank, 2, fmt="rgba8", runs=runs)
+        frs.append(f)
+    poses = ["P0", "P1", "P2", "P3"]
+    refs = []
+    for name in poses:
+        setup(R, "T", POSES[name], 128)
+        R.set_params(count_evals=0)
+        refs.append(R.render_rgba8(W, H).cpu().numpy())
+    got = []
+    for i, name in enumerate(poses):
+        for f, rr in ((frs[1], r1), (frs[0], R)):
+            setup(rr, "T", POSES[name], 128)
+            rr.set_params(count_evals=0)
+            f.submit()
+        if i > 0:
+            torch.cuda.synchronize()
+            got.append(frs[0].frame.cpu().numpy())
+    frs[1].flush()
+    got.append(frs[0].flush().cpu().numpy())
+    torch.cuda.synchronize()
+    assert len(got) == len(refs)
+    for g, ref in zip(got, refs):
+        assert np.array_equal(g, ref)
+    r1.close()
+
+
 def test_context_outlives_a_destroyed_stream(torch_cuda):
     """Completion events are recorded lazily: when the
     context leaves a stream, the event goes on that stream while it still
