@@ -415,29 +415,48 @@ class DistributedFrame:
         if self._pack_calls[slot][c] is not None:
             self._native(self._pack_calls[slot][c])
 
-    def _gather_async(self, slot, c):
-        """Start chunk c's gather (c None: every row); returns the works."""
-        import torch.distributed as dist
+    def _gather_views(self, slot, c):
+        """The tensors of chunk c's gather (c None: every row), cached per slot
+        and chunk (slicing them per frame costs host time at N = 8): for
+        point-to-point parts the (peer, tensor) pairs, else (send, gather_list)."""
+        key = (slot, c)
+        cache = self.__dict__.setdefault("_views", {})
+        if key in cache:
+            return cache[key]
         p = self.plan
-        if p.weighted:  # point-to-point: the parts differ in size
-            ops = []
+        if p.weighted:
+            pairs = []
             if self.rank == 0:
                 base = p.part_bases()
                 for q in range(1, self.world):
                     cq = self.all_cuts[q]
                     j0, j1 = (0, p.count(q)) if c is None else (cq[c], cq[c + 1])
                     if j1 > j0:
-                        ops.append(dist.P2POp(dist.irecv, self.gathered[slot][base[q] + j0: base[q] + j1], q,
-                                              group=self.group))
+                        pairs.append((q, self.gathered[slot][base[q] + j0: base[q] + j1]))
             else:
                 j0, j1 = (0, self.nmine) if c is None else (self.cuts[c], self.cuts[c + 1])
                 if j1 > j0:
-                    ops.append(dist.P2POp(dist.isend, self.wires[slot][j0:j1], 0, group=self.group))
+                    pairs.append((0, self.wires[slot][j0:j1]))
+            v = pairs
+        else:
+            j0, j1 = (0, p.rows_per_shard) if c is None else (self.cuts[c], self.cuts[c + 1])
+            g = self.gathered[slot] if self.rank == 0 else None
+            v = (self.wires[slot][j0:j1], [g[r, j0:j1] for r in range(self.world)] if self.rank == 0 else None)
+        cache[key] = v
+        return v
+
+    def _gather_async(self, slot, c):
+        """Start chunk c's gather (c None: every row); returns the works."""
+        import torch.distributed as dist
+        p = self.plan
+        v = self._gather_views(slot, c)
+        if p.weighted:  # point-to-point: the parts differ in size (the ops reused frame after frame)
+            ops = self._views.get(("ops", slot, c))
+            if ops is None:
+                op = dist.irecv if self.rank == 0 else dist.isend
+                ops = self._views[("ops", slot, c)] = [dist.P2POp(op, t, q, group=self.group) for q, t in v]
             return dist.batch_isend_irecv(ops) if ops else []
-        j0, j1 = (0, p.rows_per_shard) if c is None else (self.cuts[c], self.cuts[c + 1])
-        g = self.gathered[slot] if self.rank == 0 else None
-        glist = [g[r, j0:j1] for r in range(self.world)] if self.rank == 0 else None
-        return [dist.gather(self.wires[slot][j0:j1], gather_list=glist, dst=0, group=self.group, async_op=True)]
+        return [dist.gather(v[0], gather_list=v[1], dst=0, group=self.group, async_op=True)]
 
     def _gather_blocking(self, slot):
         """The host-staged gather (gloo), completed inside the call."""
