@@ -200,6 +200,7 @@ __device__ __forceinline__ uint32_t wire_decode_tile(uint64_t mine, int l, uint3
 
 constexpr int kDecodeTiles = 2;  // tiles per wave (1, 2, 4, 8 measured: 2 fastest, profiles/r06/decode_ab.log)
 constexpr int kDecodeWaves = 4;  // waves per workgroup (one-wave workgroups cap a CU's resident waves)
+constexpr int kDecodeWorkgroups = 7 * 256;  // the launch's target workgroup count (launch_wire_decode_parts)
 __device__ __forceinline__ void wire_decode_tiles(const uint8_t* __restrict__ msg, int n, int W, int tx0, int ty,
                                                   int cycle, int offset, int run, uint32_t* __restrict__ frame) {
     const int l = threadIdx.x & 63, TX = (W + 7) / 8;
@@ -301,7 +302,16 @@ hipError_t launch_wire_decode_parts(const WireParts& parts, int W, uint32_t* fra
     if (parts.n <= 0 || rows <= 0) return hipSuccess;
     const int TY = (rows + 7) / 8;
     const int per = kDecodeTiles * kDecodeWaves, gx = ((W + 7) / 8 + per - 1) / per;
-    hipLaunchKernelGGL(rm_wire_tile_decode_parts, dim3(gx, TY < 65535 ? TY : 65535, parts.n), dim3(64 * kDecodeWaves), 0,
+    // about seven workgroups per CU in all, each looping over tile rows
+    // (blockIdx.y strides): the decode then takes as many wave slots as one
+    // resident round and shares the CUs with the next frame's render on the
+    // other stream.  In DeltaFrame's loop the root's frame at N = 8 (C3) went
+    // 0.111-0.116 -> 0.099-0.105 ms against 2, 8, 16 or all tile rows per
+    // grid row (profiles/r06/decode_grid_ab.log); the decode alone is slower
+    // (0.042 -> 0.057 ms).
+    const int want = (kDecodeWorkgroups + gx * parts.n - 1) / (gx * parts.n);
+    const int gy = TY < want ? TY : (want < 1 ? 1 : want);
+    hipLaunchKernelGGL(rm_wire_tile_decode_parts, dim3(gx, gy, parts.n), dim3(64 * kDecodeWaves), 0,
                        s, parts, W, frame);
     return hipGetLastError();
 }
