@@ -38,6 +38,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -575,11 +576,18 @@ def main():
                 break
 
     def trial_ms(f, n=16):
-        # untimed trial: n pipelined frames, wall time, max over ranks
+        # untimed trial: pipelined frames, wall time, max over ranks; at least n
+        # frames and about 20 ms of them (the count agreed over the ranks from
+        # the warm-up frames: every rank must run the same collectives)
+        dist.barrier()
+        t0 = time.perf_counter()
         for _ in range(4):
             f.submit()
         f.flush()
         torch.cuda.synchronize(dev)
+        est = torch.tensor([(time.perf_counter() - t0) / 4 * 1e3], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(est, op=dist.ReduceOp.MAX)
+        n = int(min(256, max(n, math.ceil(20.0 / max(float(est.item()), 1e-3)))))
         dist.barrier()
         t1 = time.perf_counter()
         for _ in range(n):
@@ -641,7 +649,7 @@ def main():
                    "runs": list(fr.plan.part_runs), "wire": fr.wire,
                    "trial_ms": {k: v[1] for k, v in cands.items()}, "balanced_runs": runs, "model": model,
                    "balanced_runs_delta": runs_delta, "model_delta": model_delta,
-                   "note": "untimed trial frames (16 pipelined frames per candidate, max over ranks) before the "
+                   "note": "untimed trial frames (16-256 pipelined frames per candidate, about 20 ms, max over ranks) before the "
                            "instrumented run and the warm-up; the timed frames use the chosen candidate"}
         if errors:
             balance["errors"] = errors
