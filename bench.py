@@ -612,7 +612,7 @@ def main():
             try:
                 f = make()
                 cands[name] = (f, trial_ms(f))
-            except (RuntimeError, ValueError) as e:  # keep the others; say why in the line
+            except Exception as e:  # noqa: BLE001 -- keep the others; say why in the line (the same on every rank)
                 errors[name] = f"{type(e).__name__}: {e}"
                 torch.cuda.synchronize(dev)
 
