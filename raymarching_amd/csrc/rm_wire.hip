@@ -126,6 +126,67 @@ __global__ __launch_bounds__(256) void rm_wire_tile_compact(const uint8_t* __res
     }
 }
 
+// E2 + E3 in one launch for parts of up to kDirectTiles tiles: workgroup b
+// (tiles 256 b .. 256 b + 255, four 64-tile chunks) sums the counts of every
+// tile before it itself (8 counts per 8-byte load over its 256 lanes, then a
+// workgroup reduction) instead of reading a base a scan kernel wrote; each wave
+// adds the counts of the chunks before its own in the workgroup, scans its
+// lanes and compacts its tiles as rm_wire_tile_compact does.  The last
+// workgroup writes the message size.  (One launch less per part and frame;
+// the redundant prefix sums read T^2 / 512 bytes in all, from L2.)
+constexpr long long kDirectTiles = 65536;
+__device__ __forceinline__ uint32_t byte_sum8(uint2 v) {  // the eight bytes' sum
+    const uint32_t a = (v.x & 0x00ff00ffu) + ((v.x >> 8) & 0x00ff00ffu) + (v.y & 0x00ff00ffu) +
+                       ((v.y >> 8) & 0x00ff00ffu);
+    return (a & 0xffffu) + (a >> 16);
+}
+__global__ __launch_bounds__(256) void rm_wire_tile_compact_direct(const uint8_t* __restrict__ ws, long long T,
+                                                                   uint8_t* __restrict__ msg,
+                                                                   long long* __restrict__ size_out) {
+    __shared__ uint32_t red[4], wave_tot[4];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const uint8_t* counts = ws + wire_counts_offset(T);
+    // the counts of tiles [0, 256 b): 8-byte loads (the counts start 8-byte
+    // aligned: 200 T bytes into the workspace), strided over the lanes
+    const long long pre = 256ll * blockIdx.x, nq = pre / 8;
+    uint32_t s = 0;
+    for (long long q = tid; q < nq; q += 256) s += byte_sum8(reinterpret_cast<const uint2*>(counts)[q]);
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) s += (uint32_t)__shfl_xor((int)s, k, 64);
+    if (l == 0) red[w] = s;
+    const long long t = 256ll * blockIdx.x + tid;
+    const uint32_t cnt = t < T ? counts[t] : 0u;
+    uint32_t x = cnt;  // inclusive scan over the wave's lanes
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)x, k, 64);
+        if (l >= k) x += u;
+    }
+    if (l == 63) wave_tot[w] = x;
+    __syncthreads();
+    uint32_t off = red[0] + red[1] + red[2] + red[3] + x - cnt;
+    for (int v = 0; v < w; v++) off += wave_tot[v];
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) {
+        const uint32_t total = red[0] + red[1] + red[2] + red[3] + wave_tot[0] + wave_tot[1] + wave_tot[2] +
+                               wave_tot[3];
+        const long long bytes = (long long)wire_header_bytes(T) + 8ll * (long long)total;
+        *reinterpret_cast<long long*>(msg) = bytes;
+        if (size_out) *size_out = bytes;
+    }
+    if (t >= T) return;
+    reinterpret_cast<uint32_t*>(msg + 8)[t] = off << 5 | cnt;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(ws);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(msg + wire_header_bytes(T)) + off;
+    for (uint32_t q0 = 0; q0 < cnt; q0 += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) v[k] = q0 + k < cnt ? src[(q0 + k) * T + t] : 0ull;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++)
+            if (q0 + k < cnt) dst[q0 + k] = v[k];
+    }
+}
+
 // D: a wave rebuilds kDecodeTiles tiles (tx0 .. of tile row ty) of a part into
 // their pixels of the frame (the part's packed row j is frame row y(j): (y mod
 // cycle) - offset in [0, run)).  The table entries and then every tile's words
@@ -269,6 +330,11 @@ long long wire_workspace(int W, int n) {
 hipError_t launch_wire_finish(const void* workspace, int W, int n, uint8_t* msg, long long* size_out, hipStream_t s) {
     const long long T = (long long)((W + 7) / 8) * ((n + 7) / 8);
     const uint8_t* ws = reinterpret_cast<const uint8_t*>(workspace);
+    if (T > 0 && T <= kDirectTiles) {
+        hipLaunchKernelGGL(rm_wire_tile_compact_direct, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, ws, T,
+                           msg, size_out);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(rm_wire_tile_scan, dim3(1), dim3(1024), 0, s, ws, T, msg, size_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || T == 0) return e;
